@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident Noise transport AEAD throughput on MI355X.
+
+Metric (BASELINE.json): GiB/s device-resident AEAD encrypt+decrypt of
+64 Ki x 1400 B records per GPU.  One "step" = one seal pass (encrypt +
+Poly1305/GHASH tag) over the batch followed by one open pass (verify + decrypt)
+of the sealed batch, both through the C ABI of noise-c_amd
+(noise_aead_dev_{seal,open}_uniform).  Payload processed per step per GPU =
+2 x records x len (every byte goes through one AEAD op in each direction).
+Inputs are resident in HBM before timing; the batch sets rotate so that the
+working set (> 1 GiB) cannot be served from the 256 MiB Infinity Cache.
+
+Multi-GPU: one process per GPU (torchrun), records sharded by range with no
+data-path collective — each rank seals/opens its own 64 Ki records of the
+global stream (nonce base = rank x records): weak scaling.  Only the timing
+barrier and a max-over-ranks all_reduce use the process group.
+
+The CPU baseline is the reference noise-c itself (oracle/_ref/ref_bench: the
+reference's CipherState API compiled from its own sources), timed on this
+host's cores on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "noise-c_amd"))
+
+CHACHA, AES = 0x4301, 0x4302
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md chip table
+
+CONFIGS = {
+    # name: cipher, records per GPU, record length, key states per GPU
+    "c2": dict(cipher=CHACHA, records=65536, len=1400, states=1,
+               workload="ChaCha20-Poly1305 64Ki x 1400B records, one CipherState key"),
+    "c3": dict(cipher=AES, records=65536, len=1400, states=1,
+               workload="AES-256-GCM 64Ki x 1400B records, one CipherState key"),
+    "c4": dict(cipher=CHACHA, records=1048576, len=1400, states=4096,
+               workload="ChaCha20-Poly1305 1Mi x 1400B records, 4096 CipherStates x 256"),
+}
+IN_ALIGN = 16  # device record strides are padded to 16 B (layout)
+
+
+def shard(records_per_gpu: int, states: int, rank: int, world: int):
+    """Records of rank `rank` in the global stream (weak scaling): the rank's
+    records are [rank*R, (rank+1)*R); with S states per GPU, global state
+    rank*S + s owns records rank*R + s*(R/S) ... and its nonces start at 0.
+    With a single state per GPU the ranks share one logical CipherState whose
+    nonce runs across the ranks' ranges (nonce base = rank*R)."""
+    first = rank * records_per_gpu
+    rps = records_per_gpu // states
+    if states == 1:
+        nonce_base = [first]
+    else:
+        nonce_base = [0] * states
+    key_ids = [rank * states + s for s in range(states)] if states > 1 else [0]
+    return dict(first=first, count=records_per_gpu, rps=rps, nonce_base=nonce_base,
+                key_ids=key_ids)
+
+
+def stride(n: int) -> int:
+    return (n + IN_ALIGN - 1) // IN_ALIGN * IN_ALIGN
+
+
+def cpu_baseline(cfg, budget_cpu_s: float = 12.0):
+    """Reference noise-c (oracle/_ref/ref_bench), bounded sample."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+    kind = "reference"
+    if not os.path.exists(ref):
+        ref = os.path.join(ROOT, "oracle", "_build", "port_bench")
+        kind = "port"
+    if not os.path.exists(ref):
+        return None
+    cname = "aesgcm" if cfg["cipher"] == AES else "chachapoly"
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu))
+    # calibrate on one thread (~0.3 s), then size the sample to the budget
+    probe_n = 200 if cfg["cipher"] == AES else 2000
+    out = subprocess.run([ref, "roundtrip", cname, str(cfg["len"]), str(probe_n), "1"],
+                         capture_output=True, text=True, timeout=120, check=True)
+    p = json.loads(out.stdout)
+    rec_per_s = probe_n / max(p["seconds"], 1e-6)
+    per_thread = max(probe_n, int(rec_per_s * budget_cpu_s / threads))
+    out = subprocess.run([ref, "roundtrip", cname, str(cfg["len"]), str(per_thread),
+                          str(threads)], capture_output=True, text=True, timeout=600, check=True)
+    r = json.loads(out.stdout)
+    one = subprocess.run([ref, "roundtrip", cname, str(cfg["len"]), str(max(probe_n, int(rec_per_s * 2))), "1"],
+                         capture_output=True, text=True, timeout=120, check=True)
+    r1 = json.loads(one.stdout)
+    return {"value": round(r["gib_per_s"], 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "single_thread": round(r1["gib_per_s"], 4),
+            "sample": (f"{'noise-c ref backend CipherState API' if kind == 'reference' else 'oracle restatement'}"
+                       f" {cname}: {threads} threads x {per_thread} records x {cfg['len']} B, each "
+                       f"encrypted then decrypted+verified (send/recv CipherState pair per thread), "
+                       f"wall clock; 1 thread: {r1['gib_per_s']:.3f} GiB/s"),
+            "ok": r["ok"]}
+
+
+def load_traffic(config_name: str, kernel: str):
+    path = os.path.join(ROOT, "profiles", f"traffic_{config_name}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    k = t.get("kernels", {}).get(kernel)
+    return None if k is None else k.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per record (0 = library default)")
+    ap.add_argument("--sets", type=int, default=4, help="rotating batch sets (> MALL)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="check every open status after timing")
+    args = ap.parse_args()
+
+    import torch
+    import noise_aead as A
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfg = CONFIGS[args.config]
+    cipher, N, L, S = cfg["cipher"], cfg["records"], cfg["len"], cfg["states"]
+    sh = shard(N, S, rank, world)
+    in_stride, out_stride = stride(L), stride(L + 16)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    # keys: SplitMix64 words of seed 0x6B6579 at 4*(global key id)
+    key_ids = torch.tensor(sh["key_ids"], dtype=torch.int64)
+    raw = torch.empty(len(sh["key_ids"]) * 32, dtype=torch.uint8, device=dev)
+    for i, kid in enumerate(sh["key_ids"]):
+        assert A.dev_fill_splitmix(raw[32 * i:].data_ptr(), 32, 0x6B6579, 4 * kid, sp) == 0
+    ctx = torch.empty(len(sh["key_ids"]) * A.dev_ctx_bytes(cipher), dtype=torch.uint8, device=dev)
+    assert A.dev_prepare(cipher, raw.data_ptr(), len(sh["key_ids"]), ctx.data_ptr(), sp) == 0
+    nonce = torch.tensor(sh["nonce_base"], dtype=torch.int64, device=dev)
+    del key_ids
+
+    sets = []
+    for b in range(args.sets):
+        pt = torch.empty(N * in_stride, dtype=torch.uint8, device=dev)
+        # plaintext word w of the global stream = splitmix64(seed_pt + w)
+        word0 = (sh["first"] * in_stride + b * (1 << 40)) // 8
+        assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), 0x7074, word0, sp) == 0
+        ct = torch.empty(N * out_stride, dtype=torch.uint8, device=dev)
+        back = torch.empty(N * in_stride, dtype=torch.uint8, device=dev)
+        st = torch.empty(N, dtype=torch.uint8, device=dev)
+        sets.append((pt, ct, back, st))
+    torch.cuda.synchronize(dev)
+
+    lanes = args.lanes or A.dev_default_lanes(cipher, N)
+
+    def seal(b):
+        pt, ct, _, _ = sets[b]
+        return A.dev_uniform(False, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
+                             inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
+                             out_stride=out_stride, length=L, n_records=N,
+                             recs_per_state=sh["rps"], lanes=lanes, stream=sp)
+
+    def open_(b):
+        _, ct, back, st = sets[b]
+        return A.dev_uniform(True, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
+                             inp=ct.data_ptr(), out=back.data_ptr(), in_stride=out_stride,
+                             out_stride=in_stride, length=L, n_records=N,
+                             recs_per_state=sh["rps"], status=st.data_ptr(), lanes=lanes,
+                             stream=sp)
+
+    for w in range(args.warmup):
+        assert seal(w % args.sets) == 0
+        assert open_(w % args.sets) == 0
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        b = s % args.sets
+        ev[s][0].record(stream)
+        rc1 = seal(b)
+        ev[s][1].record(stream)
+        rc2 = open_(b)
+        ev[s][2].record(stream)
+        if rc1 or rc2:
+            raise RuntimeError(f"launch failed {rc1:#x} {rc2:#x}")
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+
+    seal_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    open_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+
+    ok = True
+    if args.verify:
+        for b in range(min(args.sets, args.steps)):
+            pt, _, back, st = sets[b]
+            ok &= bool((st == 0).all().item())
+            v = pt.view(N, in_stride)[:, :L]
+            ok &= bool(torch.equal(back.view(N, in_stride)[:, :L], v))
+
+    payload_step = 2.0 * N * L * world                         # both directions, all ranks
+    value = payload_step * args.steps / elapsed / GIB
+    alg_seal = N * (2 * L + 16) + len(sh["key_ids"]) * 40       # SURVEY §8d algorithmic bytes
+    achieved = alg_seal / (seal_ms * 1e-3) / 1e9
+    kname = "chachapoly_seal_uniform" if cipher == CHACHA else "gcm_uniform<false>"
+    traffic = load_traffic(args.config, kname)
+    result = {
+        "metric": "GiB/s device-resident AEAD encrypt+decrypt, 64Ki x 1400B records per GPU",
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (SplitMix64 plaintext and keys, SURVEY.md 8d), resident in HBM",
+        "config": {"workload": cfg["workload"], "config": args.config, "records_per_gpu": N,
+                   "record_len": L, "states_per_gpu": S, "lanes_per_record": lanes,
+                   "in_stride": in_stride, "out_stride": out_stride,
+                   "payload_bytes_per_step": int(payload_step), "parallelism": f"records x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": kname,
+                     "algorithmic_bytes_per_launch": alg_seal,
+                     "avg_launch_ms": round(seal_ms, 5)},
+        "seal_gibs": round(N * L * world / (seal_ms * 1e-3) / GIB, 2),
+        "open_gibs": round(N * L * world / (open_ms * 1e-3) / GIB, 2),
+        "open_roofline_frac": round(alg_seal / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+    }
+    if args.verify:
+        result["verified"] = ok
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(cfg)
+        except Exception as e:  # reported, never fatal to the GPU number
+            result["cpu_baseline"] = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,200 @@
+/*
+ * noise_aead_hip.h — C ABI of the MI355X (gfx950) transport AEAD engine.
+ *
+ * Drop-in for noise-c's CipherState path (rweather/noise-c v0.0.1):
+ *
+ *  1. The reference's public CipherState API, same names, signatures,
+ *     validation and error codes (include/noise/protocol/cipherstate.h:34-53,
+ *     src/protocol/cipherstate.c:77-555).  Link this library in place of the
+ *     CipherState part of libnoiseprotocol.
+ *  2. The reference's cipher plugin constructors (src/protocol/internal.h:
+ *     655-656) returning objects whose first member has the exact layout of
+ *     struct NoiseCipherState_s (internal.h:58-146), so the reference's own
+ *     cipherstate.c / symmetricstate.c keep working against them.
+ *  3. Additive batch entry points (host buffers): N records, any mix of
+ *     CipherStates, one GPU pass — results identical to N sequential calls.
+ *  4. Device-resident entry points: records, keys and nonces already in HBM.
+ *
+ * Every computation on the encrypt/decrypt path runs in the gfx950 kernels;
+ * there is no CPU fallback.  Without a usable GPU the crypto entry points
+ * return NOISE_ERROR_SYSTEM.
+ */
+#ifndef NOISE_AEAD_HIP_H
+#define NOISE_AEAD_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------- reference types/constants */
+
+#ifndef NOISE_BUFFER_H
+#define NOISE_BUFFER_H
+/* include/noise/protocol/buffer.h:33-48 */
+typedef struct {
+    uint8_t *data;
+    size_t size;
+    size_t max_size;
+} NoiseBuffer;
+#define noise_buffer_init(buffer) \
+    ((buffer).data = 0, (buffer).size = 0, (buffer).max_size = 0)
+#define noise_buffer_set_output(buffer, ptr, len) \
+    ((buffer).data = (ptr), (buffer).size = 0, (buffer).max_size = (len))
+#define noise_buffer_set_input(buffer, ptr, len) \
+    ((buffer).data = (ptr), (buffer).size = (buffer).max_size = (len))
+#define noise_buffer_set_inout(buffer, ptr, len, max) \
+    ((buffer).data = (ptr), (buffer).size = (len), (buffer).max_size = (max))
+#endif
+
+#ifndef NOISE_CONSTANTS_H
+/* include/noise/protocol/constants.h:31-38, 131-151 */
+#define NOISE_ID(ch, num) ((((int)(ch)) << 8) | ((int)(num)))
+#define NOISE_CIPHER_NONE 0
+#define NOISE_CIPHER_CATEGORY NOISE_ID('C', 0)
+#define NOISE_CIPHER_CHACHAPOLY NOISE_ID('C', 1)
+#define NOISE_CIPHER_AESGCM NOISE_ID('C', 2)
+#define NOISE_ERROR_NONE 0
+#define NOISE_ERROR_NO_MEMORY NOISE_ID('E', 1)
+#define NOISE_ERROR_UNKNOWN_ID NOISE_ID('E', 2)
+#define NOISE_ERROR_UNKNOWN_NAME NOISE_ID('E', 3)
+#define NOISE_ERROR_MAC_FAILURE NOISE_ID('E', 4)
+#define NOISE_ERROR_NOT_APPLICABLE NOISE_ID('E', 5)
+#define NOISE_ERROR_SYSTEM NOISE_ID('E', 6)
+#define NOISE_ERROR_INVALID_LENGTH NOISE_ID('E', 10)
+#define NOISE_ERROR_INVALID_PARAM NOISE_ID('E', 11)
+#define NOISE_ERROR_INVALID_STATE NOISE_ID('E', 12)
+#define NOISE_ERROR_INVALID_NONCE NOISE_ID('E', 13)
+#define NOISE_MAX_PAYLOAD_LEN 65535
+#endif
+
+/* ------------------------------------------------ 1. CipherState API
+ * Each replaces the function of the same name in src/protocol/cipherstate.c. */
+
+typedef struct NoiseCipherState_s NoiseCipherState;
+
+int noise_cipherstate_new_by_id(NoiseCipherState **state, int id);        /* cipherstate.c:77-104 */
+int noise_cipherstate_new_by_name(NoiseCipherState **state, const char *name); /* :122-140 */
+int noise_cipherstate_free(NoiseCipherState *state);                      /* :152-165 */
+int noise_cipherstate_get_cipher_id(const NoiseCipherState *state);       /* :174-177 */
+size_t noise_cipherstate_get_key_length(const NoiseCipherState *state);   /* :188-191 */
+size_t noise_cipherstate_get_mac_length(const NoiseCipherState *state);   /* :202-205 */
+int noise_cipherstate_init_key(NoiseCipherState *state, const uint8_t *key,
+                               size_t key_len);                           /* :221-235 */
+int noise_cipherstate_has_key(const NoiseCipherState *state);             /* :247-250 */
+int noise_cipherstate_encrypt_with_ad(NoiseCipherState *state, const uint8_t *ad,
+                                      size_t ad_len, NoiseBuffer *buffer); /* :293-333 */
+int noise_cipherstate_decrypt_with_ad(NoiseCipherState *state, const uint8_t *ad,
+                                      size_t ad_len, NoiseBuffer *buffer); /* :373-410 */
+int noise_cipherstate_encrypt(NoiseCipherState *state, NoiseBuffer *buffer); /* :452-455 */
+int noise_cipherstate_decrypt(NoiseCipherState *state, NoiseBuffer *buffer); /* :494-497 */
+int noise_cipherstate_set_nonce(NoiseCipherState *state, uint64_t nonce);    /* :518-535 */
+int noise_cipherstate_get_max_key_length(void);                           /* :542-545 */
+int noise_cipherstate_get_max_mac_length(void);                           /* :552-555 */
+
+/* ------------------------------------------------ 2. plugin constructors
+ * internal.h:655-656; objects start with struct NoiseCipherState_s
+ * (internal.h:58-146) filled as cipher-chachapoly.c:145-158 /
+ * cipher-aesgcm.c:190-203 do, plus a destroy hook (as the OpenSSL backend,
+ * src/backend/openssl/cipher-aesgcm.c:188-204) that frees device memory. */
+NoiseCipherState *noise_chachapoly_new(void);
+NoiseCipherState *noise_aesgcm_new(void);
+
+/* ------------------------------------------------ 3. batch (host buffers)
+ *
+ * Process count records: record i is buffers[i] under states[i] (states may
+ * repeat and may mix ciphers) with associated data ads[i]/ad_lens[i] (both
+ * arrays may be NULL for no AD).  results[i] receives exactly what
+ *   noise_cipherstate_{en,de}crypt_with_ad(states[i], ads[i], ad_lens[i], &buffers[i])
+ * would have returned had the calls been made one by one in index order, and
+ * buffers, sizes and nonces end up exactly as after those calls (including
+ * the no-key pass-through, nonce exhaustion and the "nonce not advanced on a
+ * MAC failure" rule, cipherstate.c:321-326, 400-405).  One GPU pass in the
+ * common case.  Returns NOISE_ERROR_NONE unless an argument is invalid or the
+ * GPU fails (NOISE_ERROR_SYSTEM; then results[] is unspecified). */
+int noise_cipherstate_encrypt_batch(NoiseCipherState *const *states,
+                                    const uint8_t *const *ads, const size_t *ad_lens,
+                                    NoiseBuffer *buffers, size_t count, int *results);
+int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states,
+                                    const uint8_t *const *ads, const size_t *ad_lens,
+                                    NoiseBuffer *buffers, size_t count, int *results);
+
+/* ------------------------------------------------ 4. device-resident API
+ *
+ * All pointers below are device pointers on the current HIP device; `stream`
+ * is a hipStream_t (NULL = default stream).  Calls are asynchronous.
+ *
+ * Key contexts: n_states contexts of noise_aead_dev_ctx_bytes(cipher) bytes
+ * each, built from n_states raw 32-byte keys by noise_aead_dev_prepare
+ * (ChaChaPoly: the key itself; AESGCM: round keys + GHASH tables). */
+size_t noise_aead_dev_ctx_bytes(int cipher_id);
+int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_states,
+                           void *d_ctx, void *stream);
+
+/* Uniform batch.  Record i (0 <= i < n_records) belongs to state
+ * s = i / recs_per_state and uses nonce nonce_base[s] + i % recs_per_state.
+ * seal: in + i*in_stride holds len plaintext bytes; out + i*out_stride
+ *       receives CT || tag (len + 16 bytes).
+ * open: in + i*in_stride holds CT || tag; out + i*out_stride receives the
+ *       len plaintext bytes only when the tag verifies; status[i] = 0 (ok) or
+ *       1 (MAC failure, nothing written).  in == out (in place) is allowed.
+ * lanes_per_record: 0 = automatic (ChaChaPoly 1/2/4/8; AESGCM 4). */
+typedef struct NoiseAeadUniform {
+    const void *ctx;
+    const uint64_t *nonce_base;
+    const uint8_t *in;
+    uint8_t *out;
+    const uint8_t *ad;       /* may be NULL when ad_len == 0 */
+    uint8_t *status;         /* open only; may be NULL */
+    uint64_t in_stride, out_stride, ad_stride;
+    uint32_t recs_per_state;
+    uint32_t n_records;
+    uint32_t len;            /* <= 65535 - 16 */
+    uint32_t ad_len;
+    uint32_t lanes_per_record;
+    uint32_t reserved_;
+} NoiseAeadUniform;
+
+int noise_aead_dev_seal_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream);
+int noise_aead_dev_open_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream);
+
+/* Ragged batch: one descriptor per record.  The key context of a record is
+ * at ctx_base + ctx_off (ctx_base may be NULL with absolute ctx_off). */
+typedef struct NoiseAeadRecord {
+    uint64_t in_off;
+    uint64_t out_off;
+    uint64_t nonce;
+    uint64_t ctx_off;
+    uint64_t ad_off;
+    uint32_t len;
+    uint32_t ad_len;
+} NoiseAeadRecord;
+
+typedef struct NoiseAeadRagged {
+    const void *ctx_base;
+    const NoiseAeadRecord *recs; /* device array of n_records descriptors */
+    const uint8_t *in;
+    uint8_t *out;
+    const uint8_t *ad;
+    uint8_t *status;
+    uint32_t n_records;
+    uint32_t lanes_per_record;
+} NoiseAeadRagged;
+
+int noise_aead_dev_seal_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);
+int noise_aead_dev_open_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);
+
+/* Default lanes per record the library picks for a batch of n records. */
+int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records);
+
+/* Deterministic synthetic bytes (bench/test input): 64-bit LE word w of the
+ * output = SplitMix64(seed + word0 + w), SURVEY.md §8d. */
+int noise_aead_dev_fill_splitmix(uint8_t *d_out, uint64_t nbytes, uint64_t seed,
+                                 uint64_t word0, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

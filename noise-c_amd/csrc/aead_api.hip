@@ -1,0 +1,256 @@
+/*
+ * aead_api.hip — the thin C-ABI layer between the plain-C host front end
+ * (cipherstate.c) and the gfx950 kernels.  Device-resident entry points of
+ * include/noise_aead_hip.h: plain pointers, sizes and an opaque stream; no
+ * C++ or torch types cross this boundary.  HIP errors map to
+ * NOISE_ERROR_SYSTEM (constants.h:137), bad arguments to
+ * NOISE_ERROR_INVALID_PARAM / _INVALID_LENGTH / _UNKNOWN_ID.
+ */
+#include "noise_aead_hip.h"
+#include "aead_kernels.h"
+#include <hip/hip_runtime.h>
+#include <mutex>
+
+
+#include "chachapoly.hip"
+#include "aesgcm.hip"
+
+using namespace na;
+
+namespace {
+
+constexpr int kMaxDevices = 64;
+std::once_flag g_tab_once[kMaxDevices];
+hipError_t g_tab_err[kMaxDevices];
+
+int hip_rc(hipError_t e) { return e == hipSuccess ? NOISE_ERROR_NONE : NOISE_ERROR_SYSTEM; }
+
+/* S-box / T-table are generated on each device once (aesgcm.hip). */
+hipError_t ensure_aes_tables(hipStream_t stream)
+{
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    std::call_once(g_tab_once[dev], [&] {
+        hipLaunchKernelGGL(aes_tables_init, dim3(1), dim3(256), 0, stream);
+        g_tab_err[dev] = hipGetLastError();
+        if (g_tab_err[dev] == hipSuccess) g_tab_err[dev] = hipStreamSynchronize(stream);
+    });
+    return g_tab_err[dev];
+}
+
+/* Lanes per record for ChaChaPoly: enough lanes in flight to give every
+   SIMD several waves (256 CUs x 16 waves x 64 lanes), never more than 8. */
+int auto_lanes(uint32_t n_records)
+{
+    const uint64_t target = 256ull * 16 * 64;
+    int k = 1;
+    while (k < 8 && (uint64_t)n_records * k < target) k <<= 1;
+    return k;
+}
+
+template <typename Args>
+using KernelFn = void (*)(Args);
+
+template <typename Args>
+int launch(KernelFn<Args> fn, uint32_t n_records, int lanes, const Args &a, hipStream_t s)
+{
+    if (n_records == 0) return NOISE_ERROR_NONE;
+    const uint64_t threads = (uint64_t)n_records * lanes;
+    const uint32_t blocks = (uint32_t)((threads + 255) / 256);
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, a);
+    return hip_rc(hipGetLastError());
+}
+
+KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open)
+{
+    switch (k) {
+    case 1: return open ? chachapoly_open_uniform<1> : chachapoly_seal_uniform<1>;
+    case 2: return open ? chachapoly_open_uniform<2> : chachapoly_seal_uniform<2>;
+    case 4: return open ? chachapoly_open_uniform<4> : chachapoly_seal_uniform<4>;
+    case 8: return open ? chachapoly_open_uniform<8> : chachapoly_seal_uniform<8>;
+    }
+    return nullptr;
+}
+
+KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open)
+{
+    switch (k) {
+    case 1: return open ? chachapoly_open_ragged<1> : chachapoly_seal_ragged<1>;
+    case 2: return open ? chachapoly_open_ragged<2> : chachapoly_seal_ragged<2>;
+    case 4: return open ? chachapoly_open_ragged<4> : chachapoly_seal_ragged<4>;
+    case 8: return open ? chachapoly_open_ragged<8> : chachapoly_seal_ragged<8>;
+    }
+    return nullptr;
+}
+
+int check_uniform(const NoiseAeadUniform *j)
+{
+    if (!j || !j->ctx || !j->nonce_base || !j->in || !j->out || !j->recs_per_state)
+        return NOISE_ERROR_INVALID_PARAM;
+    if (j->ad_len && !j->ad) return NOISE_ERROR_INVALID_PARAM;
+    if (j->len > NOISE_MAX_PAYLOAD_LEN - 16) return NOISE_ERROR_INVALID_LENGTH;
+    if ((uintptr_t)j->ctx & 15) return NOISE_ERROR_INVALID_PARAM;
+    return NOISE_ERROR_NONE;
+}
+
+UniformArgs to_args(const NoiseAeadUniform *j)
+{
+    UniformArgs a;
+    a.keys = (const uint8_t *)j->ctx;
+    a.nonce_base = j->nonce_base;
+    a.in = j->in;
+    a.out = j->out;
+    a.ad = j->ad;
+    a.status = j->status;
+    a.in_stride = j->in_stride;
+    a.out_stride = j->out_stride;
+    a.ad_stride = j->ad_stride;
+    a.rps = j->recs_per_state;
+    a.n_records = j->n_records;
+    a.len = j->len;
+    a.ad_len = j->ad_len;
+    return a;
+}
+
+int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool open)
+{
+    int rc = check_uniform(job);
+    if (rc) return rc;
+    hipStream_t s = (hipStream_t)stream;
+    const UniformArgs a = to_args(job);
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
+        int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records);
+        KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open);
+        if (!fn) return NOISE_ERROR_INVALID_PARAM;
+        return launch(fn, job->n_records, k, a, s);
+    }
+    if (cipher_id == NOISE_CIPHER_AESGCM) {
+        if (job->lanes_per_record && job->lanes_per_record != GCM_LANES)
+            return NOISE_ERROR_INVALID_PARAM;
+        rc = hip_rc(ensure_aes_tables(s));
+        if (rc) return rc;
+        return launch(open ? gcm_uniform<true> : gcm_uniform<false>, job->n_records,
+                      GCM_LANES, a, s);
+    }
+    return NOISE_ERROR_UNKNOWN_ID;
+}
+
+int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool open)
+{
+    if (!job || !job->recs || !job->in || !job->out) return NOISE_ERROR_INVALID_PARAM;
+    hipStream_t s = (hipStream_t)stream;
+    RaggedArgs a;
+    a.keys = (const uint8_t *)job->ctx_base;
+    a.recs = (const RecDesc *)job->recs;
+    a.in = job->in;
+    a.out = job->out;
+    a.ad = job->ad;
+    a.status = job->status;
+    a.n_records = job->n_records;
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
+        int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records);
+        KernelFn<RaggedArgs> fn = chacha_ragged_fn(k, open);
+        if (!fn) return NOISE_ERROR_INVALID_PARAM;
+        return launch(fn, job->n_records, k, a, s);
+    }
+    if (cipher_id == NOISE_CIPHER_AESGCM) {
+        int rc = hip_rc(ensure_aes_tables(s));
+        if (rc) return rc;
+        return launch(open ? gcm_ragged<true> : gcm_ragged<false>, job->n_records, GCM_LANES, a, s);
+    }
+    return NOISE_ERROR_UNKNOWN_ID;
+}
+
+__global__ void splitmix_fill(uint8_t *out, uint64_t nbytes, uint64_t seed, uint64_t word0)
+{
+    const uint64_t nw = nbytes / 8;
+    for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w * 8 < nbytes;
+         w += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = seed + word0 + w + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        if (w < nw) {
+            ((uint64_t *)out)[w] = z;
+        } else {
+            for (uint64_t b = 0; b < nbytes - 8 * w; ++b) out[8 * w + b] = (uint8_t)(z >> (8 * b));
+        }
+    }
+}
+
+} // namespace
+
+static_assert(sizeof(NoiseAeadRecord) == sizeof(RecDesc), "record descriptor layout");
+static_assert(offsetof(NoiseAeadRecord, ctx_off) == offsetof(RecDesc, ctx_off), "layout");
+
+extern "C" {
+
+size_t noise_aead_dev_ctx_bytes(int cipher_id)
+{
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) return 32;
+    if (cipher_id == NOISE_CIPHER_AESGCM) return sizeof(AesCtx);
+    return 0;
+}
+
+int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_states,
+                           void *d_ctx, void *stream)
+{
+    if (!d_raw_keys || !d_ctx) return NOISE_ERROR_INVALID_PARAM;
+    if (n_states == 0) return NOISE_ERROR_NONE;
+    hipStream_t s = (hipStream_t)stream;
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY)
+        return hip_rc(hipMemcpyAsync(d_ctx, d_raw_keys, (size_t)n_states * 32,
+                                     hipMemcpyDeviceToDevice, s));
+    if (cipher_id == NOISE_CIPHER_AESGCM) {
+        int rc = hip_rc(ensure_aes_tables(s));
+        if (rc) return rc;
+        hipLaunchKernelGGL(gcm_prepare, dim3(n_states), dim3(256), 0, s, d_raw_keys,
+                           (AesCtx *)d_ctx, n_states);
+        return hip_rc(hipGetLastError());
+    }
+    return NOISE_ERROR_UNKNOWN_ID;
+}
+
+int noise_aead_dev_seal_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream)
+{
+    return run_uniform(cipher_id, job, stream, false);
+}
+
+int noise_aead_dev_open_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream)
+{
+    return run_uniform(cipher_id, job, stream, true);
+}
+
+int noise_aead_dev_seal_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream)
+{
+    return run_ragged(cipher_id, job, stream, false);
+}
+
+int noise_aead_dev_open_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream)
+{
+    return run_ragged(cipher_id, job, stream, true);
+}
+
+int noise_aead_dev_fill_splitmix(uint8_t *d_out, uint64_t nbytes, uint64_t seed,
+                                 uint64_t word0, void *stream)
+{
+    if (!d_out) return NOISE_ERROR_INVALID_PARAM;
+    if (!nbytes) return NOISE_ERROR_NONE;
+    uint64_t words = (nbytes + 7) / 8;
+    uint32_t blocks = (uint32_t)((words + 255) / 256);
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(splitmix_fill, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_out,
+                       nbytes, seed, word0);
+    return hip_rc(hipGetLastError());
+}
+
+int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)
+{
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) return auto_lanes(n_records);
+    if (cipher_id == NOISE_CIPHER_AESGCM) return GCM_LANES;
+    return 0;
+}
+
+} // extern "C"

@@ -1,0 +1,301 @@
+/*
+ * aead_device.h — gfx950 device primitives for the transport AEADs.
+ *
+ * ChaCha20 block function (the DJB 64-bit-counter / 64-bit-IV layout of
+ * src/crypto/chacha/chacha.c:74-133), Poly1305 field arithmetic mod 2^130-5
+ * in five 26-bit limbs (the function of src/crypto/donna/poly1305-donna-64.h
+ * :101-223, re-shaped for 32-bit VALU lanes: every product is one
+ * v_mad_u64_u32), and record I/O helpers that tolerate any byte alignment.
+ *
+ * Everything here is integer VALU work; nothing touches MFMA.
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NA_DEV __device__ __forceinline__
+
+namespace na {
+
+/* ------------------------------------------------------------- ChaCha20 */
+
+NA_DEV uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+
+#define NA_QR(a, b, c, d)                \
+    a += b; d ^= a; d = rotl(d, 16);     \
+    c += d; b ^= c; b = rotl(b, 12);     \
+    a += b; d ^= a; d = rotl(d, 8);      \
+    c += d; b ^= c; b = rotl(b, 7)
+
+/* 20-round block: state words 0-3 "expand 32-byte k", 4-11 key, 12-13 the
+   64-bit block counter, 14-15 the 64-bit IV = LE64(nonce)
+   (chacha.c:74-133; cipher-chachapoly.c:62-66). */
+NA_DEV void chacha20_block(const uint32_t key[8], uint32_t ctr_lo, uint32_t ctr_hi,
+                           uint32_t iv_lo, uint32_t iv_hi, uint32_t x[16])
+{
+    x[0] = 0x61707865u; x[1] = 0x3320646eu; x[2] = 0x79622d32u; x[3] = 0x6b206574u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[4 + i] = key[i];
+    x[12] = ctr_lo; x[13] = ctr_hi; x[14] = iv_lo; x[15] = iv_hi;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        NA_QR(x[0], x[4], x[8], x[12]);  NA_QR(x[1], x[5], x[9], x[13]);
+        NA_QR(x[2], x[6], x[10], x[14]); NA_QR(x[3], x[7], x[11], x[15]);
+        NA_QR(x[0], x[5], x[10], x[15]); NA_QR(x[1], x[6], x[11], x[12]);
+        NA_QR(x[2], x[7], x[8], x[13]);  NA_QR(x[3], x[4], x[9], x[14]);
+    }
+    x[0] += 0x61707865u; x[1] += 0x3320646eu; x[2] += 0x79622d32u; x[3] += 0x6b206574u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[4 + i] += key[i];
+    x[12] += ctr_lo; x[13] += ctr_hi; x[14] += iv_lo; x[15] += iv_hi;
+}
+
+/* ------------------------------------------------------------- Poly1305 */
+
+constexpr uint32_t M26 = 0x3ffffffu;
+
+struct Fe { uint32_t l0, l1, l2, l3, l4; };          /* partially reduced */
+struct Mul { uint32_t r0, r1, r2, r3, r4, s1, s2, s3, s4; }; /* r and 5*r */
+
+NA_DEV Fe fe_zero() { return Fe{0, 0, 0, 0, 0}; }
+
+NA_DEV Mul mk_mul(const Fe &r)
+{
+    return Mul{r.l0, r.l1, r.l2, r.l3, r.l4, r.l1 * 5, r.l2 * 5, r.l3 * 5, r.l4 * 5};
+}
+
+NA_DEV Fe mul_fe(const Mul &m) { return Fe{m.r0, m.r1, m.r2, m.r3, m.r4}; }
+
+/* r from the first 16 key-stream bytes, clamped
+   (poly1305-donna-64.h:80-86 applies the same mask 0x0ffffffc0ffffffc0ffffffc0fffffff) */
+NA_DEV Fe fe_clamp_r(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3)
+{
+    return Fe{k0 & 0x3ffffffu,
+              __builtin_amdgcn_alignbit(k1, k0, 26) & 0x3ffff03u,
+              __builtin_amdgcn_alignbit(k2, k1, 20) & 0x3ffc0ffu,
+              __builtin_amdgcn_alignbit(k3, k2, 14) & 0x3f03fffu,
+              (k3 >> 8) & 0x00fffffu};
+}
+
+/* h += 16-byte block (LE words) with the 2^128 bit set; every block of the
+   AEAD's Poly input is a full, padded block (cipher-chachapoly.c:81-105), so
+   the hibit is always 1. */
+NA_DEV void fe_add_block(Fe &h, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3)
+{
+    h.l0 += w0 & M26;
+    h.l1 += __builtin_amdgcn_alignbit(w1, w0, 26) & M26;
+    h.l2 += __builtin_amdgcn_alignbit(w2, w1, 20) & M26;
+    h.l3 += __builtin_amdgcn_alignbit(w3, w2, 14) & M26;
+    h.l4 += (w3 >> 8) | (1u << 24);
+}
+
+/* h * m mod 2^130-5.  Inputs: limbs < 2^27.  Output limbs < 2^26 except l1
+   < 2^26 + 2^6.  25 v_mad_u64_u32 + carry chain. */
+NA_DEV Fe fe_mul(const Fe &h, const Mul &m)
+{
+    uint64_t d0 = (uint64_t)h.l0 * m.r0 + (uint64_t)h.l1 * m.s4 + (uint64_t)h.l2 * m.s3 +
+                  (uint64_t)h.l3 * m.s2 + (uint64_t)h.l4 * m.s1;
+    uint64_t d1 = (uint64_t)h.l0 * m.r1 + (uint64_t)h.l1 * m.r0 + (uint64_t)h.l2 * m.s4 +
+                  (uint64_t)h.l3 * m.s3 + (uint64_t)h.l4 * m.s2;
+    uint64_t d2 = (uint64_t)h.l0 * m.r2 + (uint64_t)h.l1 * m.r1 + (uint64_t)h.l2 * m.r0 +
+                  (uint64_t)h.l3 * m.s4 + (uint64_t)h.l4 * m.s3;
+    uint64_t d3 = (uint64_t)h.l0 * m.r3 + (uint64_t)h.l1 * m.r2 + (uint64_t)h.l2 * m.r1 +
+                  (uint64_t)h.l3 * m.r0 + (uint64_t)h.l4 * m.s4;
+    uint64_t d4 = (uint64_t)h.l0 * m.r4 + (uint64_t)h.l1 * m.r3 + (uint64_t)h.l2 * m.r2 +
+                  (uint64_t)h.l3 * m.r1 + (uint64_t)h.l4 * m.r0;
+    Fe o;
+    uint32_t c;
+    c = (uint32_t)(d0 >> 26); o.l0 = (uint32_t)d0 & M26;
+    d1 += c; c = (uint32_t)(d1 >> 26); o.l1 = (uint32_t)d1 & M26;
+    d2 += c; c = (uint32_t)(d2 >> 26); o.l2 = (uint32_t)d2 & M26;
+    d3 += c; c = (uint32_t)(d3 >> 26); o.l3 = (uint32_t)d3 & M26;
+    d4 += c; c = (uint32_t)(d4 >> 26); o.l4 = (uint32_t)d4 & M26;
+    o.l0 += c * 5; c = o.l0 >> 26; o.l0 &= M26; o.l1 += c;
+    return o;
+}
+
+NA_DEV Fe fe_mul(const Fe &a, const Fe &b) { return fe_mul(a, mk_mul(b)); }
+
+/* Carry-normalise limbs (each < 2^31) to < 2^26 (l1 < 2^26 + 2^6). */
+NA_DEV Fe fe_carry(Fe h)
+{
+    uint32_t c;
+    c = h.l0 >> 26; h.l0 &= M26; h.l1 += c;
+    c = h.l1 >> 26; h.l1 &= M26; h.l2 += c;
+    c = h.l2 >> 26; h.l2 &= M26; h.l3 += c;
+    c = h.l3 >> 26; h.l3 &= M26; h.l4 += c;
+    c = h.l4 >> 26; h.l4 &= M26; h.l0 += c * 5;
+    c = h.l0 >> 26; h.l0 &= M26; h.l1 += c;
+    return h;
+}
+
+/* tag = (h mod p) + s mod 2^128 (poly1305-donna-64.h:154-223 finish). */
+NA_DEV void fe_finish(Fe h, const uint32_t s[4], uint32_t tag[4])
+{
+    h = fe_carry(h);
+    uint32_t c;
+    c = h.l1 >> 26; h.l1 &= M26; h.l2 += c;
+    c = h.l2 >> 26; h.l2 &= M26; h.l3 += c;
+    c = h.l3 >> 26; h.l3 &= M26; h.l4 += c;
+    c = h.l4 >> 26; h.l4 &= M26; h.l0 += c * 5;
+    c = h.l0 >> 26; h.l0 &= M26; h.l1 += c;
+    /* g = h + 5 - 2^130; select g when h >= p */
+    uint32_t g0 = h.l0 + 5; c = g0 >> 26; g0 &= M26;
+    uint32_t g1 = h.l1 + c; c = g1 >> 26; g1 &= M26;
+    uint32_t g2 = h.l2 + c; c = g2 >> 26; g2 &= M26;
+    uint32_t g3 = h.l3 + c; c = g3 >> 26; g3 &= M26;
+    uint32_t g4 = h.l4 + c - (1u << 26);
+    uint32_t mask = (g4 >> 31) - 1u; /* all ones when g4 did not borrow */
+    h.l0 = (h.l0 & ~mask) | (g0 & mask);
+    h.l1 = (h.l1 & ~mask) | (g1 & mask);
+    h.l2 = (h.l2 & ~mask) | (g2 & mask);
+    h.l3 = (h.l3 & ~mask) | (g3 & mask);
+    h.l4 = (h.l4 & ~mask) | (g4 & mask);
+    uint32_t w0 = h.l0 | (h.l1 << 26);
+    uint32_t w1 = (h.l1 >> 6) | (h.l2 << 20);
+    uint32_t w2 = (h.l2 >> 12) | (h.l3 << 14);
+    uint32_t w3 = (h.l3 >> 18) | (h.l4 << 8);
+    uint64_t f;
+    f = (uint64_t)w0 + s[0];             tag[0] = (uint32_t)f;
+    f = (uint64_t)w1 + s[1] + (f >> 32); tag[1] = (uint32_t)f;
+    f = (uint64_t)w2 + s[2] + (f >> 32); tag[2] = (uint32_t)f;
+    f = (uint64_t)w3 + s[3] + (f >> 32); tag[3] = (uint32_t)f;
+}
+
+NA_DEV Fe fe_add(const Fe &a, const Fe &b)
+{
+    return Fe{a.l0 + b.l0, a.l1 + b.l1, a.l2 + b.l2, a.l3 + b.l3, a.l4 + b.l4};
+}
+
+NA_DEV Fe fe_select(bool c, const Fe &a, const Fe &b) { return c ? a : b; }
+
+/* Sum of a field element over an aligned group of G lanes (G | 64). */
+template <int G>
+NA_DEV Fe fe_group_sum(Fe h)
+{
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) {
+        h.l0 += (uint32_t)__shfl_xor((int)h.l0, off, 64);
+        h.l1 += (uint32_t)__shfl_xor((int)h.l1, off, 64);
+        h.l2 += (uint32_t)__shfl_xor((int)h.l2, off, 64);
+        h.l3 += (uint32_t)__shfl_xor((int)h.l3, off, 64);
+        h.l4 += (uint32_t)__shfl_xor((int)h.l4, off, 64);
+    }
+    return h;
+}
+
+/* ------------------------------------------------------------ record I/O */
+
+NA_DEV uint32_t ld_bytes(const uint8_t *p, uint32_t n) /* n in [0,4] */
+{
+    uint32_t w = 0;
+    if (n > 0) w |= (uint32_t)p[0];
+    if (n > 1) w |= (uint32_t)p[1] << 8;
+    if (n > 2) w |= (uint32_t)p[2] << 16;
+    if (n > 3) w |= (uint32_t)p[3] << 24;
+    return w;
+}
+
+NA_DEV void st_bytes(uint8_t *p, uint32_t w, uint32_t n)
+{
+    if (n > 0) p[0] = (uint8_t)w;
+    if (n > 1) p[1] = (uint8_t)(w >> 8);
+    if (n > 2) p[2] = (uint8_t)(w >> 16);
+    if (n > 3) p[3] = (uint8_t)(w >> 24);
+}
+
+/* Load 16 bytes (n valid, bytes >= n read as zero) from any alignment. */
+NA_DEV void load16(const uint8_t *p, uint32_t n, uint32_t w[4])
+{
+    const uintptr_t a = (uintptr_t)p;
+    if (n >= 16 && (a & 15) == 0) {
+        uint4 v = *(const uint4 *)p;
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else if (n >= 16 && (a & 7) == 0) {
+        uint2 v0 = *(const uint2 *)p, v1 = *(const uint2 *)(p + 8);
+        w[0] = v0.x; w[1] = v0.y; w[2] = v1.x; w[3] = v1.y;
+    } else if (n >= 16 && (a & 3) == 0) {
+        const uint32_t *q = (const uint32_t *)p;
+        w[0] = q[0]; w[1] = q[1]; w[2] = q[2]; w[3] = q[3];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int rem = (int)n - 4 * i;
+            w[i] = ld_bytes(p + 4 * i, rem <= 0 ? 0u : (rem >= 4 ? 4u : (uint32_t)rem));
+        }
+    }
+}
+
+NA_DEV void store16(uint8_t *p, uint32_t n, const uint32_t w[4])
+{
+    const uintptr_t a = (uintptr_t)p;
+    if (n >= 16 && (a & 15) == 0) {
+        *(uint4 *)p = make_uint4(w[0], w[1], w[2], w[3]);
+    } else if (n >= 16 && (a & 7) == 0) {
+        *(uint2 *)p = make_uint2(w[0], w[1]);
+        *(uint2 *)(p + 8) = make_uint2(w[2], w[3]);
+    } else if (n >= 16 && (a & 3) == 0) {
+        uint32_t *q = (uint32_t *)p;
+        q[0] = w[0]; q[1] = w[1]; q[2] = w[2]; q[3] = w[3];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            int rem = (int)n - 4 * i;
+            st_bytes(p + 4 * i, w[i], rem <= 0 ? 0u : (rem >= 4 ? 4u : (uint32_t)rem));
+        }
+    }
+}
+
+/* 64-byte unit: n valid bytes (1..64), the rest read as zero. */
+NA_DEV void load_unit(const uint8_t *p, uint32_t n, uint32_t w[16])
+{
+    if (n >= 64 && ((uintptr_t)p & 15) == 0) {
+        const uint4 *q = (const uint4 *)p;
+        uint4 v0 = q[0], v1 = q[1], v2 = q[2], v3 = q[3];
+        w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w;
+        w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
+        w[8] = v2.x; w[9] = v2.y; w[10] = v2.z; w[11] = v2.w;
+        w[12] = v3.x; w[13] = v3.y; w[14] = v3.z; w[15] = v3.w;
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        int rem = (int)n - 16 * c;
+        if (rem > 0) {
+            load16(p + 16 * c, rem >= 16 ? 16u : (uint32_t)rem, w + 4 * c);
+        } else {
+            w[4 * c] = w[4 * c + 1] = w[4 * c + 2] = w[4 * c + 3] = 0;
+        }
+    }
+}
+
+NA_DEV void store_unit(uint8_t *p, uint32_t n, const uint32_t w[16])
+{
+    if (n >= 64 && ((uintptr_t)p & 15) == 0) {
+        uint4 *q = (uint4 *)p;
+        q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        q[2] = make_uint4(w[8], w[9], w[10], w[11]);
+        q[3] = make_uint4(w[12], w[13], w[14], w[15]);
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        int rem = (int)n - 16 * c;
+        if (rem > 0) store16(p + 16 * c, rem >= 16 ? 16u : (uint32_t)rem, w + 4 * c);
+    }
+}
+
+/* Zero the bytes >= n of a 64-byte unit (Poly pads with zeros). */
+NA_DEV void mask_unit(uint32_t w[16], uint32_t n)
+{
+    if (n >= 64) return;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        int rem = (int)n - 4 * i;
+        uint32_t m = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
+        w[i] &= m;
+    }
+}
+
+} // namespace na

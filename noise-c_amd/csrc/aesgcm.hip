@@ -1,0 +1,349 @@
+/*
+ * aesgcm.hip — AES-256-GCM ("AESGCM") transport AEAD for gfx950.
+ *
+ * Replaces, for batches of records, the per-record CPU path
+ *   noise_cipherstate_{en,de}crypt_with_ad     (src/protocol/cipherstate.c:293-410)
+ *   -> noise_aesgcm_{encrypt,decrypt}         (src/backend/ref/cipher-aesgcm.c:156-188)
+ *   -> rijndaelEncrypt                        (src/crypto/aes/rijndael-alg-fst.c:854-1033)
+ *   -> ghash_update / GF128_mul               (src/crypto/ghash/ghash.c:78-206)
+ * bit for bit: J0 = 0^32 || BE64(n) || 0x00000001, data counters J0+1.., tag =
+ * E_K(J0) xor GHASH_H(AD || pad || CT || pad || BE64(8|AD|) || BE64(8|CT|)),
+ * H = E_K(0^128) (cipher-aesgcm.c:38-50, 70-90, 99-154).
+ *
+ * Decomposition: GCM_LANES = 4 lanes per record.  The record's GHASH blocks
+ * i = 0..n-1 (AD, CT, length block) are dealt round-robin, end-aligned, so
+ * lane l owns i == l + n (mod 4) and its last block has exponent 4 - l.  Each
+ * lane runs Horner with H^4, scales by H^(4-l), and the group XOR-reduces.
+ * GHASH multiplies by a per-key constant use 4-bit positional tables (32
+ * nibble positions x 16 entries per multiplier) built once per key by
+ * gcm_prepare.  The lane that owns data block d also runs its CTR block.
+ *
+ * Note: table-driven GHASH/AES on LDS/L1 is not constant-time, unlike the
+ * reference's bit-serial GF128_mul (ghash.c:85-87); see DESIGN.md.
+ */
+#include "aead_device.h"
+#include "aead_kernels.h"
+
+namespace na {
+
+__device__ uint32_t g_te0[256]; /* T-table: BE word (2s, s, s, 3s) */
+__device__ uint32_t g_sbox[256];
+__device__ int g_tables_ready;
+
+NA_DEV uint32_t xtime8(uint32_t a) { return ((a << 1) ^ ((a & 0x80) ? 0x1b : 0)) & 0xff; }
+
+NA_DEV uint32_t gf8_mul(uint32_t a, uint32_t b)
+{
+    uint32_t p = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1) p ^= a;
+        a = xtime8(a);
+        b >>= 1;
+    }
+    return p;
+}
+
+/* FIPS-197 S-box and T-table, generated on the device (inverse = x^254). */
+__global__ void aes_tables_init()
+{
+    const uint32_t x = threadIdx.x;
+    uint32_t inv = 1, base = x;
+    for (int e = 254; e; e >>= 1) {
+        if (e & 1) inv = gf8_mul(inv, base);
+        base = gf8_mul(base, base);
+    }
+    if (x == 0) inv = 0;
+    uint32_t s = inv;
+    for (int i = 1; i <= 4; ++i) s ^= ((inv << i) | (inv >> (8 - i))) & 0xff;
+    s ^= 0x63;
+    g_sbox[x] = s;
+    const uint32_t s2 = xtime8(s), s3 = s2 ^ s;
+    g_te0[x] = (s2 << 24) | (s << 16) | (s << 8) | s3;
+    if (x == 0) g_tables_ready = 1;
+}
+
+NA_DEV uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+/* AES-256 encryption of one block in big-endian-word form (the GETU32/PUTU32
+   convention of rijndael-alg-fst.c:718-721). te/sb live in LDS. */
+NA_DEV void aes256_block(const uint32_t *__restrict__ rk, const uint32_t *te, const uint32_t *sb,
+                         uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3)
+{
+    s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+        const uint32_t t0 = te[s0 >> 24] ^ rotr(te[(s1 >> 16) & 255], 8) ^
+                            rotr(te[(s2 >> 8) & 255], 16) ^ rotr(te[s3 & 255], 24) ^ rk[4 * r];
+        const uint32_t t1 = te[s1 >> 24] ^ rotr(te[(s2 >> 16) & 255], 8) ^
+                            rotr(te[(s3 >> 8) & 255], 16) ^ rotr(te[s0 & 255], 24) ^ rk[4 * r + 1];
+        const uint32_t t2 = te[s2 >> 24] ^ rotr(te[(s3 >> 16) & 255], 8) ^
+                            rotr(te[(s0 >> 8) & 255], 16) ^ rotr(te[s1 & 255], 24) ^ rk[4 * r + 2];
+        const uint32_t t3 = te[s3 >> 24] ^ rotr(te[(s0 >> 16) & 255], 8) ^
+                            rotr(te[(s1 >> 8) & 255], 16) ^ rotr(te[s2 & 255], 24) ^ rk[4 * r + 3];
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint32_t o0 = (sb[s0 >> 24] << 24) | (sb[(s1 >> 16) & 255] << 16) |
+                        (sb[(s2 >> 8) & 255] << 8) | sb[s3 & 255];
+    const uint32_t o1 = (sb[s1 >> 24] << 24) | (sb[(s2 >> 16) & 255] << 16) |
+                        (sb[(s3 >> 8) & 255] << 8) | sb[s0 & 255];
+    const uint32_t o2 = (sb[s2 >> 24] << 24) | (sb[(s3 >> 16) & 255] << 16) |
+                        (sb[(s0 >> 8) & 255] << 8) | sb[s1 & 255];
+    const uint32_t o3 = (sb[s3 >> 24] << 24) | (sb[(s0 >> 16) & 255] << 16) |
+                        (sb[(s1 >> 8) & 255] << 8) | sb[s2 & 255];
+    s0 = o0 ^ rk[56]; s1 = o1 ^ rk[57]; s2 = o2 ^ rk[58]; s3 = o3 ^ rk[59];
+}
+
+/* E_K(0^32 || BE64(n) || BE32(ctr)) as little-endian memory words. */
+NA_DEV void aes_ctr_block(const uint32_t *rk, const uint32_t *te, const uint32_t *sb,
+                          uint64_t n, uint32_t ctr, uint32_t ks[4])
+{
+    uint32_t s0 = 0, s1 = (uint32_t)(n >> 32), s2 = (uint32_t)n, s3 = ctr;
+    aes256_block(rk, te, sb, s0, s1, s2, s3);
+    ks[0] = __builtin_bswap32(s0); ks[1] = __builtin_bswap32(s1);
+    ks[2] = __builtin_bswap32(s2); ks[3] = __builtin_bswap32(s3);
+}
+
+/* y <- y * Y where tab is Y's 4-bit positional table (LE-word layout). */
+NA_DEV void gh_mul(uint32_t y[4], const uint4 *__restrict__ tab)
+{
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+#pragma unroll
+    for (int p = 0; p < 32; ++p) {
+        const int b = p >> 1;
+        const int sh = 8 * (b & 3) + ((p & 1) ? 0 : 4);
+        const uint32_t v = (y[b >> 2] >> sh) & 15u;
+        const uint4 e = tab[p * 16 + v];
+        r0 ^= e.x; r1 ^= e.y; r2 ^= e.z; r3 ^= e.w;
+    }
+    y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
+}
+
+/* ----------------------------------------------------------- key prepare */
+
+/* Byte-serial GF(2^128) helpers for the (once per key) table build. */
+NA_DEV void gf_mulx(uint8_t v[16])
+{
+    const uint8_t carry = v[15] & 1;
+    for (int j = 15; j > 0; --j) v[j] = (uint8_t)((v[j] >> 1) | (v[j - 1] << 7));
+    v[0] >>= 1;
+    if (carry) v[0] ^= 0xE1;
+}
+
+NA_DEV void gf_mul_bytes(const uint8_t x[16], const uint8_t h[16], uint8_t out[16])
+{
+    uint8_t z[16] = {0}, v[16];
+    for (int j = 0; j < 16; ++j) v[j] = h[j];
+    for (int i = 0; i < 128; ++i) {
+        if ((x[i >> 3] >> (7 - (i & 7))) & 1)
+            for (int j = 0; j < 16; ++j) z[j] ^= v[j];
+        gf_mulx(v);
+    }
+    for (int j = 0; j < 16; ++j) out[j] = z[j];
+}
+
+/* One workgroup per state: round keys, H, and the H^1..H^4 tables. */
+__global__ __launch_bounds__(256) void gcm_prepare(const uint8_t *__restrict__ raw_keys,
+                                                   AesCtx *__restrict__ ctx, uint32_t n_states)
+{
+    __shared__ uint32_t te[256], sb[256], rk[60];
+    __shared__ uint8_t hp[GCM_LANES][16];       /* H^1..H^4, bytes */
+    __shared__ uint8_t V[GCM_LANES][128][16];   /* x^i * H^m */
+    const uint32_t st = blockIdx.x;
+    if (st >= n_states) return;
+    const int t = threadIdx.x;
+    te[t] = g_te0[t];
+    sb[t] = g_sbox[t];
+    __syncthreads();
+    if (t == 0) {
+        const uint8_t *k = raw_keys + (size_t)st * 32;
+        for (int i = 0; i < 8; ++i)
+            rk[i] = ((uint32_t)k[4 * i] << 24) | ((uint32_t)k[4 * i + 1] << 16) |
+                    ((uint32_t)k[4 * i + 2] << 8) | k[4 * i + 3];
+        uint32_t rcon = 1;
+        for (int i = 8; i < 60; ++i) {
+            uint32_t tmp = rk[i - 1];
+            if (i % 8 == 0) {
+                tmp = (tmp << 8) | (tmp >> 24); /* RotWord */
+                tmp = (sb[tmp >> 24] << 24) | (sb[(tmp >> 16) & 255] << 16) |
+                      (sb[(tmp >> 8) & 255] << 8) | sb[tmp & 255];
+                tmp ^= rcon << 24;
+                rcon = xtime8(rcon);
+            } else if (i % 8 == 4) {
+                tmp = (sb[tmp >> 24] << 24) | (sb[(tmp >> 16) & 255] << 16) |
+                      (sb[(tmp >> 8) & 255] << 8) | sb[tmp & 255];
+            }
+            rk[i] = rk[i - 8] ^ tmp;
+        }
+        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        aes256_block(rk, te, sb, s0, s1, s2, s3);
+        const uint32_t hw[4] = {s0, s1, s2, s3};
+        for (int i = 0; i < 16; ++i) hp[0][i] = (uint8_t)(hw[i >> 2] >> (24 - 8 * (i & 3)));
+        for (int m = 1; m < GCM_LANES; ++m) gf_mul_bytes(hp[m - 1], hp[0], hp[m]);
+    }
+    __syncthreads();
+    if (t < GCM_LANES) {
+        uint8_t v[16];
+        for (int j = 0; j < 16; ++j) v[j] = hp[t][j];
+        for (int i = 0; i < 128; ++i) {
+            for (int j = 0; j < 16; ++j) V[t][i][j] = v[j];
+            gf_mulx(v);
+        }
+    }
+    __syncthreads();
+    AesCtx *c = ctx + st;
+    if (t < 60) c->rk[t] = rk[t];
+    if (t < 4) {
+        uint32_t w = 0;
+        for (int j = 0; j < 4; ++j) w |= (uint32_t)hp[0][4 * t + j] << (8 * j);
+        c->h[t] = w;
+    }
+    for (int e = t; e < GCM_LANES * GHASH_TAB_ENTRIES; e += 256) {
+        const int m = e / GHASH_TAB_ENTRIES, p = (e / 16) % 32, val = e % 16;
+        uint8_t acc[16] = {0};
+        for (int bit = 0; bit < 4; ++bit)
+            if ((val >> (3 - bit)) & 1)
+                for (int j = 0; j < 16; ++j) acc[j] ^= V[m][4 * p + bit][j];
+        for (int w = 0; w < 4; ++w)
+            c->tab[m][p * 16 + val][w] = (uint32_t)acc[4 * w] | ((uint32_t)acc[4 * w + 1] << 8) |
+                                         ((uint32_t)acc[4 * w + 2] << 16) |
+                                         ((uint32_t)acc[4 * w + 3] << 24);
+    }
+}
+
+/* ---------------------------------------------------------------- records */
+
+struct GcmView {
+    const uint8_t *src;
+    uint8_t *dst;
+    const uint8_t *ad;
+    const AesCtx *ctx;
+    uint64_t nonce;
+    uint32_t len, ad_len;
+};
+
+/* Returns (seal) true; (open) whether the tag verified. */
+template <bool OPEN>
+NA_DEV bool gcm_record(const GcmView &rv, int l, const uint32_t *te, const uint32_t *sb)
+{
+    constexpr int K = GCM_LANES;
+    const AesCtx *ctx = rv.ctx;
+    const uint32_t *rk = ctx->rk;
+    const uint32_t A = (rv.ad_len + 15) / 16, M = (rv.len + 15) / 16;
+    const uint32_t n = A + M + 1;
+    const uint32_t c0 = ((uint32_t)l + n) % K;
+    const uint4 *tabH4 = (const uint4 *)ctx->tab[K - 1];
+    uint32_t acc[4] = {0, 0, 0, 0};
+    for (uint32_t i = c0; i < n; i += K) {
+        if (i != c0) gh_mul(acc, tabH4);
+        uint32_t x[4];
+        if (i < A) {
+            const uint32_t rem = rv.ad_len - 16 * i;
+            load16(rv.ad + 16 * i, rem >= 16 ? 16u : rem, x);
+        } else if (i < A + M) {
+            const uint32_t d = i - A;
+            const uint32_t rem = rv.len - 16 * d;
+            const uint32_t nb = rem >= 16 ? 16u : rem;
+            load16(rv.src + 16 * d, nb, x);
+            if (!OPEN) {
+                uint32_t ks[4];
+                aes_ctr_block(rk, te, sb, rv.nonce, 2 + d, ks);
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const int rb = (int)nb - 4 * w;
+                    const uint32_t m = rb >= 4 ? 0xffffffffu : (rb <= 0 ? 0u : ((1u << (8 * rb)) - 1u));
+                    x[w] = (x[w] ^ ks[w]) & m;
+                }
+                store16(rv.dst + 16 * d, nb, x);
+            }
+        } else {
+            const uint64_t ab = (uint64_t)rv.ad_len * 8, cb = (uint64_t)rv.len * 8;
+            x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
+            x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
+        }
+        acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
+    }
+    /* scale by H^(K-l) (lane l's last block has exponent K-l) */
+    gh_mul(acc, (const uint4 *)ctx->tab[K - 1 - l]);
+#pragma unroll
+    for (int off = 1; off < K; off <<= 1)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+    /* tag = E_K(J0) xor S: every lane of the group computes it (one AES) */
+    uint32_t ej[4];
+    aes_ctr_block(rk, te, sb, rv.nonce, 1u, ej);
+    uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
+    if (!OPEN) {
+        if (l == K - 1) store16(rv.dst + rv.len, 16, tag);
+        return true;
+    }
+    uint32_t got[4];
+    load16(rv.src + rv.len, 16, got);
+    const uint32_t diff = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
+    if (diff) return false; /* cipher-aesgcm.c:184-186: nothing decrypted */
+    for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
+        const uint32_t rem = rv.len - 16 * d;
+        const uint32_t nb = rem >= 16 ? 16u : rem;
+        uint32_t x[4], ks[4];
+        load16(rv.src + 16 * d, nb, x);
+        aes_ctr_block(rk, te, sb, rv.nonce, 2 + d, ks);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+        store16(rv.dst + 16 * d, nb, x);
+    }
+    return true;
+}
+
+NA_DEV void load_aes_tables(uint32_t *te, uint32_t *sb)
+{
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        te[i] = g_te0[i];
+        sb[i] = g_sbox[i];
+    }
+    __syncthreads();
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(256) void gcm_uniform(UniformArgs a)
+{
+    __shared__ uint32_t te[256], sb[256];
+    load_aes_tables(te, sb);
+    const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t rec = gtid / GCM_LANES;
+    if (rec >= a.n_records) return;
+    const int l = (int)(gtid % GCM_LANES);
+    const uint32_t st = rec / a.rps;
+    GcmView rv;
+    rv.src = a.in + (size_t)rec * a.in_stride;
+    rv.dst = a.out + (size_t)rec * a.out_stride;
+    rv.ad = a.ad ? a.ad + (size_t)rec * a.ad_stride : nullptr;
+    rv.ctx = (const AesCtx *)a.keys + st;
+    rv.nonce = a.nonce_base[st] + (uint64_t)(rec - st * a.rps);
+    rv.len = a.len;
+    rv.ad_len = a.ad_len;
+    const bool ok = gcm_record<OPEN>(rv, l, te, sb);
+    if (OPEN && l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
+{
+    __shared__ uint32_t te[256], sb[256];
+    load_aes_tables(te, sb);
+    const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t rec = gtid / GCM_LANES;
+    if (rec >= a.n_records) return;
+    const int l = (int)(gtid % GCM_LANES);
+    const RecDesc d = a.recs[rec];
+    GcmView rv;
+    rv.src = a.in + d.in_off;
+    rv.dst = a.out + d.out_off;
+    rv.ad = a.ad ? a.ad + d.ad_off : nullptr;
+    rv.ctx = (const AesCtx *)((uintptr_t)a.keys + d.ctx_off);
+    rv.nonce = d.nonce;
+    rv.len = d.len;
+    rv.ad_len = d.ad_len;
+    const bool ok = gcm_record<OPEN>(rv, l, te, sb);
+    if (OPEN && l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+}
+
+} // namespace na

@@ -1,0 +1,516 @@
+"""GPU parity: the gfx950 kernels, called through the C ABI, against the oracle.
+
+Bit-exact comparisons (integer/byte work): every ciphertext byte and tag must
+equal the CPU oracle's (oracle/noise_oracle.c, itself pinned to the reference
+by tests/test_oracle.py), and every decrypt must reproduce the reference's
+accept/reject decision and leave rejected records untouched.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CHACHA, AES = 0x4301, 0x4302
+NONCE_MAX = 2**64 - 1
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def dev(arr):
+    torch = _torch()
+    return torch.from_numpy(np.ascontiguousarray(arr)).to("cuda")
+
+
+def stream():
+    return _torch().cuda.current_stream().cuda_stream
+
+
+def sync():
+    _torch().cuda.synchronize()
+
+
+def prepare(aead, cipher, keys):
+    torch = _torch()
+    keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 32)
+    d_keys = dev(keys.reshape(-1))
+    ctx = torch.empty(keys.shape[0] * aead.dev_ctx_bytes(cipher), dtype=torch.uint8, device="cuda")
+    assert aead.dev_prepare(cipher, d_keys.data_ptr(), keys.shape[0], ctx.data_ptr(), stream()) == 0
+    return ctx, d_keys
+
+
+def gpu_uniform(aead, open_, cipher, keys, nonce_base, rps, inp, in_stride, length, count,
+                out_stride, lanes=0, ad=None, ad_stride=0, ad_len=0, out_init=0xA5, out=None):
+    torch = _torch()
+    ctx, _k = prepare(aead, cipher, keys)
+    d_nb = dev(np.asarray(nonce_base, dtype=np.uint64).view(np.int64))
+    d_in = dev(inp)
+    if out is None:
+        d_out = torch.full((count * out_stride + 64,), out_init, dtype=torch.uint8, device="cuda")
+    else:
+        d_out = out
+    d_st = torch.full((max(1, count),), 7, dtype=torch.uint8, device="cuda")
+    d_ad = dev(ad) if ad is not None else None
+    rc = aead.dev_uniform(open_, cipher, ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(),
+                          inp=d_in.data_ptr(), out=d_out.data_ptr(), in_stride=in_stride,
+                          out_stride=out_stride, length=length, n_records=count,
+                          recs_per_state=rps, status=d_st.data_ptr(),
+                          ad=d_ad.data_ptr() if d_ad is not None else 0, ad_stride=ad_stride,
+                          ad_len=ad_len, lanes=lanes, stream=stream())
+    assert rc == 0, hex(rc)
+    sync()
+    return d_out.cpu().numpy(), d_st.cpu().numpy()[:count]
+
+
+def oracle_seal_records(oracle, cipher, keys, nonce_base, rps, pt, in_stride, length, count,
+                        out_stride, ad=None, ad_stride=0, ad_len=0):
+    out = np.full(count * out_stride + 64, 0xA5, dtype=np.uint8)
+    for i in range(count):
+        s = i // rps
+        p = bytes(pt[i * in_stride: i * in_stride + length])
+        a = bytes(ad[i * ad_stride: i * ad_stride + ad_len]) if ad_len else b""
+        ct = oracle.encrypt(cipher, bytes(keys[s]), int(nonce_base[s]) + i % rps, p, a)
+        out[i * out_stride: i * out_stride + length + 16] = np.frombuffer(ct, dtype=np.uint8)
+    return out
+
+
+# ------------------------------------------------------------------ KATs
+
+def test_kat_through_device_api(aead, gpu, golden):
+    kat, _ = golden
+    for v in kat["vectors"]:
+        key = np.frombuffer(bytes.fromhex(v["key"]), dtype=np.uint8).reshape(1, 32)
+        pt = bytes.fromhex(v["pt"])
+        ad = bytes.fromhex(v["ad"])
+        L = len(pt)
+        inp = np.frombuffer(pt + bytes(16), dtype=np.uint8)
+        adv = np.frombuffer(ad or b"\0", dtype=np.uint8)
+        out, _ = gpu_uniform(aead, False, v["cipher"], key, [v["nonce"]], 1, inp, L + 16, L, 1,
+                             L + 16, ad=adv, ad_stride=len(ad), ad_len=len(ad))
+        assert bytes(out[:L + 16]).hex() == v["ct"] + v["tag"], v["name"]
+        back, st = gpu_uniform(aead, True, v["cipher"], key, [v["nonce"]], 1, out[:L + 16],
+                               L + 16, L, 1, L + 16, ad=adv, ad_stride=len(ad), ad_len=len(ad))
+        assert st[0] == 0 and bytes(back[:L]) == pt, v["name"]
+
+
+# --------------------------------------------------- uniform vs the oracle
+
+LENS = [0, 1, 15, 16, 17, 48, 56, 63, 64, 65, 127, 128, 129, 191, 192, 255, 256, 257,
+        1023, 1400, 1401, 4096, 5000]
+
+
+@pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 2), (CHACHA, 4), (CHACHA, 8),
+                                          (AES, 0)])
+@pytest.mark.parametrize("packed", [False, True])
+def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed):
+    rng = np.random.default_rng(1000 + lanes + 7 * packed + (cipher & 3))
+    for L in LENS:
+        count, rps = 37, 13  # 3 states, the last one partial
+        S = (count + rps - 1) // rps
+        keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
+        nb = rng.integers(0, 2**63, S, dtype=np.uint64) * 2
+        in_stride = L if packed else (L + 15) // 16 * 16 + 16
+        out_stride = L + 16 if packed else (L + 16 + 15) // 16 * 16
+        pt = rng.integers(0, 256, count * in_stride + 16, dtype=np.uint8)
+        exp = oracle_seal_records(oracle, cipher, keys, nb, rps, pt, in_stride, L, count, out_stride)
+        got, _ = gpu_uniform(aead, False, cipher, keys, nb, rps, pt, in_stride, L, count,
+                             out_stride, lanes=lanes)
+        assert np.array_equal(got, exp), f"seal mismatch len={L}"
+        # open it back; tamper with a few records
+        ct = got.copy()
+        bad = sorted(set(rng.integers(0, count, 5).tolist()))
+        for b in bad:
+            pos = b * out_stride + int(rng.integers(0, L + 16))
+            ct[pos] ^= 1 << int(rng.integers(0, 8))
+        back, st = gpu_uniform(aead, True, cipher, keys, nb, rps, ct, out_stride, L, count,
+                               in_stride, lanes=lanes, out_init=0x5A)
+        for i in range(count):
+            seg = back[i * in_stride: i * in_stride + L]
+            if i in bad:
+                assert st[i] == 1, f"tamper not detected len={L} rec={i}"
+                assert np.all(seg == 0x5A), "rejected record was written"
+            else:
+                assert st[i] == 0, f"valid record rejected len={L} rec={i}"
+                assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L])
+
+
+@pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 4), (CHACHA, 8), (AES, 0)])
+def test_uniform_with_ad(aead, gpu, oracle, cipher, lanes):
+    rng = np.random.default_rng(77 + lanes)
+    for L in [0, 1, 64, 65, 1024, 1400]:
+        for adl in [1, 12, 16, 32, 33, 100]:
+            count, rps = 9, 4
+            S = 3
+            keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
+            nb = rng.integers(0, 2**40, S, dtype=np.uint64)
+            stride = L + 16
+            pt = rng.integers(0, 256, count * stride + 16, dtype=np.uint8)
+            ad = rng.integers(0, 256, count * 128, dtype=np.uint8)
+            exp = oracle_seal_records(oracle, cipher, keys, nb, rps, pt, stride, L, count, stride,
+                                      ad=ad, ad_stride=128, ad_len=adl)
+            got, _ = gpu_uniform(aead, False, cipher, keys, nb, rps, pt, stride, L, count, stride,
+                                 lanes=lanes, ad=ad, ad_stride=128, ad_len=adl)
+            assert np.array_equal(got, exp), f"len={L} ad={adl}"
+            back, st = gpu_uniform(aead, True, cipher, keys, nb, rps, got, stride, L, count,
+                                   stride, lanes=lanes, ad=ad, ad_stride=128, ad_len=adl)
+            assert np.all(st == 0)
+
+
+def test_nonce_edges(aead, gpu, oracle):
+    rng = np.random.default_rng(5)
+    for cipher in (CHACHA, AES):
+        for base in [0, 2**32 - 2, 2**32 - 1, 2**63, NONCE_MAX - 4]:
+            count, L = 3, 200
+            keys = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+            pt = rng.integers(0, 256, count * L, dtype=np.uint8)
+            exp = oracle_seal_records(oracle, cipher, keys, [base], count, pt, L, L, count, L + 16)
+            got, _ = gpu_uniform(aead, False, cipher, keys, [base], count, pt, L, L, count, L + 16)
+            assert np.array_equal(got, exp), hex(base)
+
+
+def test_max_record(aead, gpu, oracle):
+    """NOISE_MAX_PAYLOAD_LEN - 16 bytes of plaintext (constants.h:151)."""
+    rng = np.random.default_rng(9)
+    L = 65535 - 16
+    for cipher, lanes in [(CHACHA, 8), (CHACHA, 1), (AES, 0)]:
+        keys = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+        pt = rng.integers(0, 256, 2 * L, dtype=np.uint8)
+        exp = oracle_seal_records(oracle, cipher, keys, [123], 2, pt, L, L, 2, L + 16)
+        got, _ = gpu_uniform(aead, False, cipher, keys, [123], 2, pt, L, L, 2, L + 16, lanes=lanes)
+        assert np.array_equal(got, exp)
+
+
+def test_in_place(aead, gpu, oracle):
+    """in == out, as the reference encrypts/decrypts the buffer in place."""
+    rng = np.random.default_rng(11)
+    for cipher in (CHACHA, AES):
+        L, count, stride = 1400, 50, 1424
+        keys = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+        pt = rng.integers(0, 256, count * stride, dtype=np.uint8)
+        exp = oracle_seal_records(oracle, cipher, keys, [0], count, pt, stride, L, count, stride)
+        ctx, _k = prepare(aead, cipher, keys)
+        d_nb = dev(np.zeros(1, dtype=np.int64))
+        buf = dev(pt)
+        rc = aead.dev_uniform(False, cipher, ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(),
+                              inp=buf.data_ptr(), out=buf.data_ptr(), in_stride=stride,
+                              out_stride=stride, length=L, n_records=count, recs_per_state=count,
+                              stream=stream())
+        assert rc == 0
+        sync()
+        g = buf.cpu().numpy()
+        for i in range(count):
+            assert np.array_equal(g[i * stride: i * stride + L + 16],
+                                  exp[i * stride: i * stride + L + 16])
+        rc = aead.dev_uniform(True, cipher, ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(),
+                              inp=buf.data_ptr(), out=buf.data_ptr(), in_stride=stride,
+                              out_stride=stride, length=L, n_records=count, recs_per_state=count,
+                              stream=stream())
+        assert rc == 0
+        sync()
+        g = buf.cpu().numpy()
+        for i in range(count):
+            assert np.array_equal(g[i * stride: i * stride + L], pt[i * stride: i * stride + L])
+
+
+# ------------------------------------------------------------ ragged kernel
+
+@pytest.mark.parametrize("cipher", [CHACHA, AES])
+def test_ragged_vs_oracle(aead, gpu, oracle, cipher):
+    rng = np.random.default_rng(21 + (cipher & 3))
+    S, count = 5, 200
+    keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
+    torch = _torch()
+    ctx, _k = prepare(aead, cipher, keys)
+    cb = aead.dev_ctx_bytes(cipher)
+    lens = rng.integers(0, 3000, count)
+    lens[:10] = [0, 1, 15, 16, 17, 63, 64, 65, 1400, 16384]
+    adls = rng.choice([0, 0, 0, 5, 32], count)
+    recs = np.zeros(count, dtype=[("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"),
+                                  ("ctx_off", "<u8"), ("ad_off", "<u8"), ("len", "<u4"),
+                                  ("ad_len", "<u4")])
+    inp_size = int(sum(int(l) + 16 + 3 for l in lens)) + 64
+    inp = rng.integers(0, 256, inp_size, dtype=np.uint8)
+    ad = rng.integers(0, 256, count * 64, dtype=np.uint8)
+    off = 0
+    exp = np.full(inp_size, 0xA5, dtype=np.uint8)
+    for i in range(count):
+        s = int(rng.integers(0, S))
+        n = int(rng.integers(0, 2**62))
+        recs[i] = (off + 3 * (i % 2), off, n, s * cb, 64 * i, lens[i], adls[i])
+        # in_off deliberately misaligned for odd records (read from off+3)
+        p = bytes(inp[off + 3 * (i % 2): off + 3 * (i % 2) + lens[i]])
+        a = bytes(ad[64 * i: 64 * i + adls[i]])
+        ct = oracle.encrypt(cipher, bytes(keys[s]), n, p, a)
+        exp[off: off + lens[i] + 16] = np.frombuffer(ct, dtype=np.uint8)
+        off += int(lens[i]) + 16 + 3
+    d_recs = dev(recs.view(np.uint8))
+    d_in, d_ad = dev(inp), dev(ad)
+    d_out = torch.full((inp_size,), 0xA5, dtype=torch.uint8, device="cuda")
+    rc = aead.dev_ragged(False, cipher, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
+                         inp=d_in.data_ptr(), out=d_out.data_ptr(), n_records=count,
+                         ad=d_ad.data_ptr(), stream=stream())
+    assert rc == 0
+    sync()
+    got = d_out.cpu().numpy()
+    assert np.array_equal(got[:off], exp[:off])
+    # open: out -> in positions swapped
+    recs2 = recs.copy()
+    recs2["in_off"], recs2["out_off"] = recs["out_off"], recs["out_off"]
+    d_recs2 = dev(recs2.view(np.uint8))
+    d_st = torch.full((count,), 9, dtype=torch.uint8, device="cuda")
+    rc = aead.dev_ragged(True, cipher, ctx_base=ctx.data_ptr(), recs=d_recs2.data_ptr(),
+                         inp=d_out.data_ptr(), out=d_out.data_ptr(), n_records=count,
+                         ad=d_ad.data_ptr(), status=d_st.data_ptr(), stream=stream())
+    assert rc == 0
+    sync()
+    assert np.all(d_st.cpu().numpy() == 0)
+    back = d_out.cpu().numpy()
+    for i in range(count):
+        o, io, L = int(recs["out_off"][i]), int(recs["in_off"][i]), int(lens[i])
+        assert np.array_equal(back[o: o + L], inp[io: io + L])
+
+
+# ------------------------------------------- the CipherState API on the GPU
+
+def test_golden_grid_through_cipherstate(aead, gpu, oracle, golden):
+    """All 500 reference-generated grid vectors through the single-record API."""
+    _, grid = golden
+    for c in grid["cases"]:
+        rc, st = aead.CipherState.new_by_id(c["cipher"])
+        assert rc == 0
+        assert st.init_key(bytes.fromhex(c["key"])) == 0
+        if c["nonce"]:
+            assert st.set_nonce(c["nonce"]) == 0
+        pt = oracle.fill(grid["seed_pt"], c["len"], c["pt_word0"])
+        ad = oracle.fill(grid["seed_ad"], c["ad_len"], c["ad_word0"])
+        out = st.seal(pt, ad)
+        assert out[-16:].hex() == c["tag"], c
+        if "ct" in c:
+            assert out[:-16].hex() == c["ct"]
+        import hashlib
+        assert hashlib.sha256(out).hexdigest() == c["sha256"]
+        st2 = aead.CipherState.new_by_id(c["cipher"])[1]
+        st2.init_key(bytes.fromhex(c["key"]))
+        if c["nonce"]:
+            st2.set_nonce(c["nonce"])
+        rc, back = st2.open(out, ad)
+        assert rc == 0 and back == pt
+        st.free()
+        st2.free()
+
+
+def _model_seq(oracle, ops):
+    """Sequential semantics of cipherstate.c:293-410 on the oracle."""
+    res = []
+    for (m, kind, ad, data, size, max_size) in ops:
+        data = bytearray(data)
+        if kind == "enc":
+            if size > max_size:
+                res.append((0x450A, bytes(data), size)); continue
+            if not m["has_key"]:
+                res.append((0x450A if size > 65535 else 0, bytes(data), size)); continue
+            if size > 65535 - 16 or max_size - size < 16:
+                res.append((0x450A, bytes(data), size)); continue
+            if m["n"] == NONCE_MAX:
+                res.append((0x450D, bytes(data), size)); continue
+            ct = oracle.encrypt(m["cipher"], m["key"], m["n"], bytes(data[:size]), ad)
+            m["n"] += 1
+            data[:size + 16] = ct
+            res.append((0, bytes(data), size + 16))
+        else:
+            if size > max_size or size > 65535:
+                res.append((0x450A, bytes(data), size)); continue
+            if not m["has_key"]:
+                res.append((0, bytes(data), size)); continue
+            if size < 16:
+                res.append((0x450A, bytes(data), size)); continue
+            if m["n"] == NONCE_MAX:
+                res.append((0x450D, bytes(data), size)); continue
+            rc, pt = oracle.decrypt(m["cipher"], m["key"], m["n"], bytes(data[:size]), ad)
+            if rc:
+                res.append((0x4504, bytes(data), size)); continue
+            m["n"] += 1
+            data[:size - 16] = pt
+            res.append((0, bytes(data), size - 16))
+    return res
+
+
+def test_batch_equals_sequential(aead, gpu, oracle):
+    """encrypt_batch / decrypt_batch == the same calls made one by one,
+    including no-key pass-through, bad lengths, MAC failures (nonce not
+    advanced) and mixed ciphers (cipherstate.c:293-410)."""
+    rng = np.random.default_rng(3)
+    n_states = 6
+    models, states = [], []
+    for s in range(n_states):
+        cipher = CHACHA if s % 2 == 0 else AES
+        st = aead.CipherState.new_by_id(cipher)[1]
+        key = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        m = dict(cipher=cipher, key=key, has_key=s != 5, n=0)
+        if m["has_key"]:
+            st.init_key(key)
+            n0 = int(rng.integers(0, 1000)) if s != 4 else NONCE_MAX - 3
+            st.set_nonce(n0)
+            m["n"] = n0
+        models.append(m)
+        states.append(st)
+    # encrypt batch
+    N = 60
+    rec_state = rng.integers(0, n_states, N)
+    mems, bufs, ads, ops = [], [], [], []
+    for i in range(N):
+        L = int(rng.choice([0, 5, 64, 100, 1400, 65535 - 16, 65535 - 15]))
+        max_size = L + 16 if rng.random() > 0.1 else L + 3
+        data = bytes(rng.integers(0, 256, L, dtype=np.uint8)) + bytes(max_size - L)
+        mem = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+        mems.append(mem)
+        bufs.append(aead.NoiseBuffer.inout(mem, L, max_size))
+        ad = bytes(rng.integers(0, 256, int(rng.choice([0, 0, 13])), dtype=np.uint8))
+        ads.append(ad)
+        ops.append((models[rec_state[i]], "enc", ad, data, L, max_size))
+    exp = _model_seq(oracle, ops)
+    rc, res = aead.encrypt_batch([states[s] for s in rec_state], bufs, ads)
+    assert rc == 0
+    for i in range(N):
+        assert res[i] == exp[i][0], (i, hex(res[i]), hex(exp[i][0]))
+        assert bufs[i].size == exp[i][2]
+        assert bytes(mems[i])[:len(exp[i][1])] == exp[i][1][:len(bytes(mems[i]))]
+    # decrypt the successful ones back with fresh states, corrupting some
+    dstates, dmodels = [], []
+    for s in range(n_states):
+        st = aead.CipherState.new_by_id(models[s]["cipher"])[1]
+        m = dict(models[s])
+        if m["has_key"]:
+            st.init_key(m["key"])
+            n0 = m["n"] - int(sum(1 for i in range(N) if rec_state[i] == s and exp[i][0] == 0))
+            st.set_nonce(n0)
+            m["n"] = n0
+        dstates.append(st)
+        dmodels.append(m)
+    dmems, dbufs, dops, dst = [], [], [], []
+    for i in range(N):
+        if exp[i][0] != 0:
+            continue
+        data = bytearray(exp[i][1][:exp[i][2]])
+        if len(data) and rng.random() < 0.15:
+            data[int(rng.integers(0, len(data)))] ^= 0x40
+        mem = (C.c_uint8 * max(1, len(data))).from_buffer_copy(bytes(data) or b"\0")
+        dmems.append(mem)
+        dbufs.append(aead.NoiseBuffer.input(mem, len(data)))
+        dops.append((dmodels[rec_state[i]], "dec", ads[i], bytes(data), len(data), len(data)))
+        dst.append(dstates[rec_state[i]])
+    dexp = _model_seq(oracle, dops)
+    rc, dres = aead.decrypt_batch(dst, dbufs, [o[2] for o in dops])
+    assert rc == 0
+    for k in range(len(dops)):
+        assert dres[k] == dexp[k][0], (k, hex(dres[k]), hex(dexp[k][0]))
+        assert dbufs[k].size == dexp[k][2]
+        assert bytes(dmems[k])[:dexp[k][2]] == dexp[k][1][:dexp[k][2]]
+    for s in states + dstates:
+        s.free()
+
+
+def test_reference_unit_suite_on_gpu(aead, gpu, golden):
+    """tests/unit/test-cipherstate.c:31-224 check_cipher, re-stated on our API."""
+    kat, _ = golden
+    names = {CHACHA: "ChaChaPoly", AES: "AESGCM"}
+    for v in kat["vectors"]:
+        cid, key = v["cipher"], bytes.fromhex(v["key"])
+        pt, ct, tag, ad = (bytes.fromhex(v[x]) for x in ("pt", "ct", "tag", "ad"))
+        nonce = v["nonce"]
+        rc, st = aead.CipherState.new_by_id(cid)
+        assert rc == 0 and st.cipher_id == cid and st.key_length == 32 and st.mac_length == 16
+        assert not st.has_key
+        buf = (C.c_uint8 * 512)()
+        C.memmove(buf, pt, len(pt))
+        nb = aead.NoiseBuffer.inout(buf, len(pt), 512)
+        assert st.encrypt_with_ad(ad, nb) == 0 and nb.size == len(pt)
+        assert bytes(buf)[:len(pt)] == pt
+        assert st.set_nonce(nonce) == 0x450C  # INVALID_STATE before a key
+        assert st.init_key(key) == 0 and st.set_nonce(nonce) == 0 and st.has_key
+        nb = aead.NoiseBuffer.inout(buf, len(pt), 512)
+        assert st.encrypt_with_ad(ad, nb) == 0 and nb.size == len(pt) + 16
+        assert bytes(buf)[:len(pt)] == ct and bytes(buf)[len(pt):len(pt) + 16] == tag
+        nb = aead.NoiseBuffer.input(buf, len(pt) + 16)
+        assert st.decrypt_with_ad(ad, nb) == 0x4504  # nonce moved on
+        assert st.set_nonce(nonce) == 0x450D
+        assert st.set_nonce(NONCE_MAX - 1) == 0
+        nb = aead.NoiseBuffer.inout(buf, len(pt), 512)
+        assert st.encrypt_with_ad(ad, nb) == 0
+        nb = aead.NoiseBuffer.inout(buf, len(pt), 512)
+        assert st.encrypt_with_ad(ad, nb) == 0x450D
+        assert st.init_key(key) == 0 and st.set_nonce(nonce) == 0
+        C.memmove(buf, ct + tag, len(ct) + 16)
+        nb = aead.NoiseBuffer.input(buf, len(pt) + 16)
+        assert st.decrypt_with_ad(ad, nb) == 0 and nb.size == len(pt)
+        assert bytes(buf)[:len(pt)] == pt
+        assert st.set_nonce(NONCE_MAX - 1) == 0
+        nb = aead.NoiseBuffer.input(buf, len(pt) + 16)
+        assert st.decrypt_with_ad(ad, nb) == 0x4504
+        nb = aead.NoiseBuffer.input(buf, len(pt) + 16)
+        assert st.decrypt_with_ad(ad, nb) == 0x4504
+        assert st.free() == 0
+        rc, st = aead.CipherState.new_by_name(names[cid])
+        assert rc == 0 and st.cipher_id == cid
+        st.free()
+
+
+# ------------------------------------- full BASELINE sizes: size-free checks
+
+@pytest.mark.parametrize("cipher", [CHACHA, AES])
+def test_full_size_config(aead, gpu, oracle, cipher):
+    """Config 2/3 shape (64 Ki x 1400 B, one key): every lane split gives the
+    same bytes, a sample of records equals the oracle, the open round trip
+    restores every plaintext and flags exactly the tampered records."""
+    torch = _torch()
+    N, L = 65536, 1400
+    in_stride, out_stride = 1408, 1424
+    key = np.arange(32, dtype=np.uint8).reshape(1, 32)
+    ctx, _k = prepare(aead, cipher, key)
+    d_nb = dev(np.array([5], dtype=np.int64))
+    d_pt = torch.empty(N * in_stride, dtype=torch.uint8, device="cuda")
+    assert aead.dev_fill_splitmix(d_pt.data_ptr(), N * in_stride, 0x5EED, 0, stream()) == 0
+    outs = []
+    lane_opts = [1, 2, 4, 8] if cipher == CHACHA else [0]
+    for lanes in lane_opts:
+        d_ct = torch.zeros(N * out_stride, dtype=torch.uint8, device="cuda")
+        rc = aead.dev_uniform(False, cipher, ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(),
+                              inp=d_pt.data_ptr(), out=d_ct.data_ptr(), in_stride=in_stride,
+                              out_stride=out_stride, length=L, n_records=N, recs_per_state=N,
+                              lanes=lanes, stream=stream())
+        assert rc == 0
+        outs.append(d_ct)
+    sync()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    ct = outs[0]
+    pt_h = d_pt.cpu().numpy()
+    ct_h = ct.cpu().numpy()
+    rng = np.random.default_rng(2)
+    for i in list(rng.integers(0, N, 64)) + [0, N - 1]:
+        i = int(i)
+        exp = oracle.encrypt(cipher, bytes(key[0]), 5 + i, bytes(pt_h[i * in_stride: i * in_stride + L]))
+        assert bytes(ct_h[i * out_stride: i * out_stride + L + 16]) == exp, i
+    bad = sorted(set(int(x) for x in rng.integers(0, N, 100)))
+    for b in bad:
+        ct[b * out_stride + int(rng.integers(0, L + 16))] ^= 0x01
+    d_back = torch.zeros(N * in_stride, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((N,), 9, dtype=torch.uint8, device="cuda")
+    rc = aead.dev_uniform(True, cipher, ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(),
+                          inp=ct.data_ptr(), out=d_back.data_ptr(), in_stride=out_stride,
+                          out_stride=in_stride, length=L, n_records=N, recs_per_state=N,
+                          status=d_st.data_ptr(), stream=stream())
+    assert rc == 0
+    sync()
+    st = d_st.cpu().numpy()
+    assert sorted(np.nonzero(st)[0].tolist()) == bad
+    mask = np.ones(N, dtype=bool)
+    mask[bad] = False
+    back = d_back.cpu().numpy().reshape(N, in_stride)[:, :L]
+    assert np.array_equal(back[mask], pt_h.reshape(N, in_stride)[:, :L][mask])
+    assert np.all(back[~mask] == 0)
