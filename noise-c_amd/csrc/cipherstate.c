@@ -142,6 +142,7 @@ static Staging *stage_get(size_t bytes)
    (the reference cleans its scratch the same way, cipher-chachapoly.c:72). */
 static void stage_scrub(void)
 {
+    pthread_once(&g_stage_once, stage_key_init);
     Staging *s = (Staging *)pthread_getspecific(g_stage_key);
     if (s && s->h && s->scrub_len) clean(s->h + s->scrub_off, s->scrub_len);
     if (s) s->scrub_len = 0;

@@ -1,0 +1,180 @@
+"""The C-ABI library: it loads, exports every symbol include/*.h declares, its
+structs have the documented layout, and the CipherState front end's host-side
+rules (validation, nonce bookkeeping, error codes — src/protocol/cipherstate.c)
+hold.  Nothing here launches a kernel: paths that would reach the GPU are not
+called on CPU."""
+import ctypes as C
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NONCE_MAX = 2**64 - 1
+
+
+@pytest.fixture(scope="module")
+def L(aead_built):
+    return aead_built.lib()
+
+
+@pytest.fixture(scope="module")
+def aead_built():
+    import noise_aead
+    if not os.path.exists(noise_aead.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "noise-c_amd")], check=True)
+    return noise_aead
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(noise_\w+)\s*\(", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_exports_every_declared_symbol(L):
+    names = declared_functions()
+    assert len(names) >= 27
+    so = os.path.join(ROOT, "noise-c_amd", "lib", "libnoise_aead_hip.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = names - exported
+    assert not missing, missing
+    for n in names:
+        assert hasattr(L, n)
+
+
+def test_struct_layouts(aead_built):
+    A = aead_built
+    assert C.sizeof(A.NoiseAeadRecord) == 48
+    assert C.sizeof(A.NoiseBuffer) == 24
+    assert C.sizeof(A.NoiseAeadUniform) == 6 * 8 + 3 * 8 + 6 * 4
+    assert A.dev_ctx_bytes(A.CHACHAPOLY) == 32
+    assert A.dev_ctx_bytes(A.AESGCM) >= 240 + 16
+    assert A.dev_ctx_bytes(0x4303) == 0
+
+
+def test_cipherstate_errors(aead_built):
+    """tests/unit/test-cipherstate.c:284-311 cipherstate_check_errors."""
+    A = aead_built
+    L = A.lib()
+    assert L.noise_cipherstate_free(None) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_get_cipher_id(None) == A.CIPHER_NONE
+    assert L.noise_cipherstate_get_key_length(None) == 0
+    assert L.noise_cipherstate_get_mac_length(None) == 0
+    assert L.noise_cipherstate_new_by_id(None, A.HASH_BLAKE2s) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_new_by_name(None, b"ChaChaPoly") == A.ERROR_INVALID_PARAM
+    p = C.c_void_p(8)
+    assert L.noise_cipherstate_new_by_id(C.byref(p), A.HASH_BLAKE2s) == A.ERROR_UNKNOWN_ID
+    assert p.value is None
+    p = C.c_void_p(8)
+    assert L.noise_cipherstate_new_by_name(C.byref(p), None) == A.ERROR_INVALID_PARAM
+    assert p.value is None
+    p = C.c_void_p(8)
+    assert L.noise_cipherstate_new_by_name(C.byref(p), b"ChaChaPony") == A.ERROR_UNKNOWN_NAME
+    assert p.value is None
+    assert L.noise_cipherstate_get_max_key_length() == 32
+    assert L.noise_cipherstate_get_max_mac_length() == 16
+
+
+@pytest.mark.parametrize("cid,name", [(0x4301, "ChaChaPoly"), (0x4302, "AESGCM")])
+def test_cipherstate_host_rules(aead_built, cid, name):
+    """The parts of check_cipher (test-cipherstate.c:31-224) that never reach
+    the GPU: properties, no-key pass-through, key/nonce rules, bad args."""
+    A = aead_built
+    rc, st = A.CipherState.new_by_id(cid)
+    assert rc == 0 and st.cipher_id == cid and st.key_length == 32 and st.mac_length == 16
+    assert not st.has_key
+    mem = (C.c_uint8 * 512)(*range(256), *range(256))
+    before = bytes(mem)
+    nb = A.NoiseBuffer.inout(mem, 100, 512)
+    assert st.encrypt_with_ad(b"ad", nb) == 0 and nb.size == 100 and bytes(mem) == before
+    nb = A.NoiseBuffer.input(mem, A.MAX_PAYLOAD_LEN + 1)
+    assert st.encrypt_with_ad(b"ad", nb) == A.ERROR_INVALID_LENGTH
+    nb = A.NoiseBuffer.inout(mem, 8, 512)
+    assert st.encrypt_with_ad(b"ad", nb) == 0 and nb.size == 8
+    nb = A.NoiseBuffer.input(mem, 116)
+    assert st.decrypt_with_ad(b"ad", nb) == 0 and nb.size == 116
+    nb = A.NoiseBuffer.input(mem, A.MAX_PAYLOAD_LEN + 1)
+    assert st.decrypt_with_ad(b"ad", nb) == A.ERROR_INVALID_LENGTH
+    nb = A.NoiseBuffer.input(mem, 8)
+    assert st.decrypt_with_ad(b"ad", nb) == 0 and nb.size == 8
+    assert st.set_nonce(5) == A.ERROR_INVALID_STATE
+    key = bytes(range(32))
+    assert st.init_key(key) == 0 and st.has_key
+    assert st.set_nonce(5) == 0
+    assert st.set_nonce(4) == A.ERROR_INVALID_NONCE
+    assert st.set_nonce(NONCE_MAX) == 0
+    # exhausted nonce: rejected before any GPU work (cipherstate.c:321-322, 394-395)
+    nb = A.NoiseBuffer.inout(mem, 10, 512)
+    assert st.encrypt_with_ad(None, nb) == A.ERROR_INVALID_NONCE
+    nb = A.NoiseBuffer.input(mem, 40)
+    assert st.decrypt_with_ad(None, nb) == A.ERROR_INVALID_NONCE
+    # size checks with a key (cipherstate.c:312-315, 389-390)
+    nb = A.NoiseBuffer.inout(mem, 65535 - 15, 65535 + 1)
+    assert st.encrypt_with_ad(None, nb) == A.ERROR_INVALID_LENGTH
+    nb = A.NoiseBuffer.inout(mem, 500, 510)
+    assert st.encrypt_with_ad(None, nb) == A.ERROR_INVALID_LENGTH
+    nb = A.NoiseBuffer.input(mem, 8)
+    assert st.decrypt_with_ad(None, nb) == A.ERROR_INVALID_LENGTH
+    nb = A.NoiseBuffer.inout(mem, 20, 10)
+    assert st.encrypt_with_ad(None, nb) == A.ERROR_INVALID_LENGTH
+    # re-keying resets the nonce (cipherstate.c:231-233)
+    assert st.init_key(key) == 0 and st.set_nonce(0) == 0
+    # parameter errors
+    L = A.lib()
+    k = (C.c_uint8 * 33)()
+    assert L.noise_cipherstate_init_key(None, k, 32) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_init_key(st.ptr, None, 32) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_init_key(st.ptr, k, 31) == A.ERROR_INVALID_LENGTH
+    assert L.noise_cipherstate_init_key(st.ptr, k, 33) == A.ERROR_INVALID_LENGTH
+    assert L.noise_cipherstate_set_nonce(None, 1) == A.ERROR_INVALID_PARAM
+    nb = A.NoiseBuffer.inout(mem, 10, 512)
+    assert L.noise_cipherstate_encrypt_with_ad(None, None, 0, C.byref(nb)) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_encrypt_with_ad(st.ptr, None, 3, C.byref(nb)) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_encrypt_with_ad(st.ptr, None, 0, None) == A.ERROR_INVALID_PARAM
+    nb.data = None
+    assert L.noise_cipherstate_encrypt_with_ad(st.ptr, None, 0, C.byref(nb)) == A.ERROR_INVALID_PARAM
+    nb = A.NoiseBuffer.input(mem, 40)
+    assert L.noise_cipherstate_decrypt_with_ad(None, None, 0, C.byref(nb)) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_decrypt_with_ad(st.ptr, None, 3, C.byref(nb)) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_decrypt_with_ad(st.ptr, None, 0, None) == A.ERROR_INVALID_PARAM
+    assert st.free() == 0
+    rc, st = A.CipherState.new_by_name(name)
+    assert rc == 0 and st.cipher_id == cid and not st.has_key
+    assert st.free() == 0
+
+
+def test_batch_host_rules(aead_built):
+    """Batch entry points: argument errors and the records that never reach
+    the GPU (no key, bad length, exhausted nonce) give per-record codes equal
+    to the single-call ones."""
+    A = aead_built
+    L = A.lib()
+    assert L.noise_cipherstate_encrypt_batch(None, None, None, None, 1, None) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_decrypt_batch(None, None, None, None, 1, None) == A.ERROR_INVALID_PARAM
+    assert L.noise_cipherstate_encrypt_batch(None, None, None, None, 0, None) == 0
+    nokey = A.CipherState.new_by_id(A.CHACHAPOLY)[1]
+    spent = A.CipherState.new_by_id(A.AESGCM)[1]
+    spent.init_key(bytes(32))
+    spent.set_nonce(NONCE_MAX)
+    mems = [(C.c_uint8 * 64)() for _ in range(4)]
+    bufs = [A.NoiseBuffer.inout(mems[0], 10, 64), A.NoiseBuffer.inout(mems[1], 60, 64),
+            A.NoiseBuffer.inout(mems[2], 10, 64), A.NoiseBuffer.inout(mems[3], 70, 64)]
+    rc, res = A.encrypt_batch([nokey, spent, spent, nokey], bufs)
+    assert rc == 0
+    assert res == [0, A.ERROR_INVALID_LENGTH, A.ERROR_INVALID_NONCE, A.ERROR_INVALID_LENGTH]
+    assert [b.size for b in bufs] == [10, 60, 10, 70]
+    bufs = [A.NoiseBuffer.input(mems[0], 40), A.NoiseBuffer.input(mems[1], 8),
+            A.NoiseBuffer.input(mems[2], 40)]
+    rc, res = A.decrypt_batch([nokey, spent, spent], bufs)
+    assert rc == 0 and res == [0, A.ERROR_INVALID_LENGTH, A.ERROR_INVALID_NONCE]
+    nokey.free()
+    spent.free()
