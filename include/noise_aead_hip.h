@@ -181,7 +181,15 @@ typedef struct NoiseAeadRagged {
     uint8_t *status;
     uint32_t n_records;
     uint32_t lanes_per_record;
+    uint32_t flags;              /* NOISE_AEAD_FLAG_* */
+    uint32_t reserved_;
 } NoiseAeadRagged;
+
+/* The caller guarantees, for every record: in + in_off and out + out_off are
+ * 16-byte aligned, and the input may be read up to roundup64(max(len, 1))
+ * bytes (and holds CT || tag for open).  Enables the straight-line dwordx4 path.  The
+ * uniform API derives this itself from the pointers and strides. */
+#define NOISE_AEAD_FLAG_FAST 1u
 
 int noise_aead_dev_seal_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);
 int noise_aead_dev_open_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);

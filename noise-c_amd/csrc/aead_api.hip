@@ -63,26 +63,51 @@ int launch(KernelFn<Args> fn, uint32_t n_records, int lanes, const Args &a, hipS
     return hip_rc(hipGetLastError());
 }
 
-KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open)
+template <bool FAST>
+KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open)
 {
     switch (k) {
-    case 1: return open ? chachapoly_open_uniform<1> : chachapoly_seal_uniform<1>;
-    case 2: return open ? chachapoly_open_uniform<2> : chachapoly_seal_uniform<2>;
-    case 4: return open ? chachapoly_open_uniform<4> : chachapoly_seal_uniform<4>;
-    case 8: return open ? chachapoly_open_uniform<8> : chachapoly_seal_uniform<8>;
+    case 1: return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
+    case 2: return open ? chachapoly_open_uniform<2, FAST> : chachapoly_seal_uniform<2, FAST>;
+    case 4: return open ? chachapoly_open_uniform<4, FAST> : chachapoly_seal_uniform<4, FAST>;
+    case 8: return open ? chachapoly_open_uniform<8, FAST> : chachapoly_seal_uniform<8, FAST>;
     }
     return nullptr;
 }
 
-KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open)
+KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast)
+{
+    return fast ? chacha_uniform_fn_t<true>(k, open) : chacha_uniform_fn_t<false>(k, open);
+}
+
+template <bool FAST>
+KernelFn<RaggedArgs> chacha_ragged_fn_t(int k, bool open)
 {
     switch (k) {
-    case 1: return open ? chachapoly_open_ragged<1> : chachapoly_seal_ragged<1>;
-    case 2: return open ? chachapoly_open_ragged<2> : chachapoly_seal_ragged<2>;
-    case 4: return open ? chachapoly_open_ragged<4> : chachapoly_seal_ragged<4>;
-    case 8: return open ? chachapoly_open_ragged<8> : chachapoly_seal_ragged<8>;
+    case 1: return open ? chachapoly_open_ragged<1, FAST> : chachapoly_seal_ragged<1, FAST>;
+    case 2: return open ? chachapoly_open_ragged<2, FAST> : chachapoly_seal_ragged<2, FAST>;
+    case 4: return open ? chachapoly_open_ragged<4, FAST> : chachapoly_seal_ragged<4, FAST>;
+    case 8: return open ? chachapoly_open_ragged<8, FAST> : chachapoly_seal_ragged<8, FAST>;
     }
     return nullptr;
+}
+
+KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open, bool fast)
+{
+    return fast ? chacha_ragged_fn_t<true>(k, open) : chacha_ragged_fn_t<false>(k, open);
+}
+
+/* FAST layout (chachapoly.hip): 16-B aligned record slots whose input may be
+   read up to roundup64(len) — and, for open, holds CT || tag. */
+bool uniform_fast(const NoiseAeadUniform *j, bool open)
+{
+    const uint64_t a = (uint64_t)(uintptr_t)j->in | (uint64_t)(uintptr_t)j->out |
+                       j->in_stride | j->out_stride;
+    if (a & 15) return false;
+    const uint64_t need = ((uint64_t)(j->len ? j->len : 1) + 63) & ~63ull;
+    if (j->in_stride < need) return false;
+    if (open && j->in_stride < (uint64_t)j->len + 16) return false;
+    return true;
 }
 
 int check_uniform(const NoiseAeadUniform *j)
@@ -122,7 +147,7 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     const UniformArgs a = to_args(job);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records);
-        KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open);
+        KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open));
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
         return launch(fn, job->n_records, k, a, s);
     }
@@ -151,7 +176,8 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
     a.n_records = job->n_records;
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records);
-        KernelFn<RaggedArgs> fn = chacha_ragged_fn(k, open);
+        KernelFn<RaggedArgs> fn =
+            chacha_ragged_fn(k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
         return launch(fn, job->n_records, k, a, s);
     }

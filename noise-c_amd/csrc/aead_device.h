@@ -93,23 +93,29 @@ NA_DEV void fe_add_block(Fe &h, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t 
    < 2^26 + 2^6.  25 v_mad_u64_u32 + carry chain. */
 NA_DEV Fe fe_mul(const Fe &h, const Mul &m)
 {
-    uint64_t d0 = (uint64_t)h.l0 * m.r0 + (uint64_t)h.l1 * m.s4 + (uint64_t)h.l2 * m.s3 +
-                  (uint64_t)h.l3 * m.s2 + (uint64_t)h.l4 * m.s1;
-    uint64_t d1 = (uint64_t)h.l0 * m.r1 + (uint64_t)h.l1 * m.r0 + (uint64_t)h.l2 * m.s4 +
-                  (uint64_t)h.l3 * m.s3 + (uint64_t)h.l4 * m.s2;
-    uint64_t d2 = (uint64_t)h.l0 * m.r2 + (uint64_t)h.l1 * m.r1 + (uint64_t)h.l2 * m.r0 +
-                  (uint64_t)h.l3 * m.s4 + (uint64_t)h.l4 * m.s3;
-    uint64_t d3 = (uint64_t)h.l0 * m.r3 + (uint64_t)h.l1 * m.r2 + (uint64_t)h.l2 * m.r1 +
-                  (uint64_t)h.l3 * m.r0 + (uint64_t)h.l4 * m.s4;
-    uint64_t d4 = (uint64_t)h.l0 * m.r4 + (uint64_t)h.l1 * m.r3 + (uint64_t)h.l2 * m.r2 +
-                  (uint64_t)h.l3 * m.r1 + (uint64_t)h.l4 * m.r0;
+    /* Each column's carry seeds the next column's v_mad_u64_u32 chain, so no
+       64-bit add or shift is needed (d_i < 2^58, so d_i >> 26 fits 32 bits). */
     Fe o;
-    uint32_t c;
-    c = (uint32_t)(d0 >> 26); o.l0 = (uint32_t)d0 & M26;
-    d1 += c; c = (uint32_t)(d1 >> 26); o.l1 = (uint32_t)d1 & M26;
-    d2 += c; c = (uint32_t)(d2 >> 26); o.l2 = (uint32_t)d2 & M26;
-    d3 += c; c = (uint32_t)(d3 >> 26); o.l3 = (uint32_t)d3 & M26;
-    d4 += c; c = (uint32_t)(d4 >> 26); o.l4 = (uint32_t)d4 & M26;
+    uint64_t d = (uint64_t)h.l0 * m.r0 + (uint64_t)h.l1 * m.s4 + (uint64_t)h.l2 * m.s3 +
+                 (uint64_t)h.l3 * m.s2 + (uint64_t)h.l4 * m.s1;
+    o.l0 = (uint32_t)d & M26;
+    d = (uint64_t)__builtin_amdgcn_alignbit((uint32_t)(d >> 32), (uint32_t)d, 26) +
+        (uint64_t)h.l0 * m.r1 + (uint64_t)h.l1 * m.r0 + (uint64_t)h.l2 * m.s4 +
+        (uint64_t)h.l3 * m.s3 + (uint64_t)h.l4 * m.s2;
+    o.l1 = (uint32_t)d & M26;
+    d = (uint64_t)__builtin_amdgcn_alignbit((uint32_t)(d >> 32), (uint32_t)d, 26) +
+        (uint64_t)h.l0 * m.r2 + (uint64_t)h.l1 * m.r1 + (uint64_t)h.l2 * m.r0 +
+        (uint64_t)h.l3 * m.s4 + (uint64_t)h.l4 * m.s3;
+    o.l2 = (uint32_t)d & M26;
+    d = (uint64_t)__builtin_amdgcn_alignbit((uint32_t)(d >> 32), (uint32_t)d, 26) +
+        (uint64_t)h.l0 * m.r3 + (uint64_t)h.l1 * m.r2 + (uint64_t)h.l2 * m.r1 +
+        (uint64_t)h.l3 * m.r0 + (uint64_t)h.l4 * m.s4;
+    o.l3 = (uint32_t)d & M26;
+    d = (uint64_t)__builtin_amdgcn_alignbit((uint32_t)(d >> 32), (uint32_t)d, 26) +
+        (uint64_t)h.l0 * m.r4 + (uint64_t)h.l1 * m.r3 + (uint64_t)h.l2 * m.r2 +
+        (uint64_t)h.l3 * m.r1 + (uint64_t)h.l4 * m.r0;
+    o.l4 = (uint32_t)d & M26;
+    uint32_t c = __builtin_amdgcn_alignbit((uint32_t)(d >> 32), (uint32_t)d, 26);
     o.l0 += c * 5; c = o.l0 >> 26; o.l0 &= M26; o.l1 += c;
     return o;
 }
@@ -182,6 +188,89 @@ NA_DEV Fe fe_group_sum(Fe h)
         h.l4 += (uint32_t)__shfl_xor((int)h.l4, off, 64);
     }
     return h;
+}
+
+/* ------------------------------------------- Poly1305, radix 2^32 Horner
+ *
+ * The hot Horner step h = (h + m + 2^128) * r with the CLAMPED r only: the
+ * clamp (top 4 bits of each r word clear, low 2 bits of r1..r3 clear) is what
+ * lets 32-bit words work — every product h_i * r_j < 2^60, a column of five
+ * fits 64 bits, and r_j * 2^128 == (5 r_j / 4) mod p for j >= 1.  20
+ * v_mad_u64_u32 and no limb splitting of the message words. */
+
+struct P32 { uint32_t h0, h1, h2, h3, h4; };        /* h4 <= 7 */
+struct R32 { uint32_t r0, r1, r2, r3, s1, s2, s3; }; /* s_j = r_j + r_j/4 */
+
+NA_DEV P32 p32_zero() { return P32{0, 0, 0, 0, 0}; }
+
+NA_DEV R32 r32_from_key(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3)
+{
+    R32 r;
+    r.r0 = k0 & 0x0fffffffu;
+    r.r1 = k1 & 0x0ffffffcu;
+    r.r2 = k2 & 0x0ffffffcu;
+    r.r3 = k3 & 0x0ffffffcu;
+    r.s1 = r.r1 + (r.r1 >> 2);
+    r.s2 = r.r2 + (r.r2 >> 2);
+    r.s3 = r.r3 + (r.r3 >> 2);
+    return r;
+}
+
+NA_DEV void p32_block(P32 &h, const R32 &r, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3)
+{
+    uint64_t t = (uint64_t)h.h0 + m0;
+    const uint32_t a0 = (uint32_t)t;
+    t = (uint64_t)h.h1 + m1 + (t >> 32);
+    const uint32_t a1 = (uint32_t)t;
+    t = (uint64_t)h.h2 + m2 + (t >> 32);
+    const uint32_t a2 = (uint32_t)t;
+    t = (uint64_t)h.h3 + m3 + (t >> 32);
+    const uint32_t a3 = (uint32_t)t;
+    const uint32_t a4 = h.h4 + (uint32_t)(t >> 32) + 1u; /* the 2^128 pad bit */
+    uint64_t d0 = (uint64_t)a0 * r.r0 + (uint64_t)a1 * r.s3 + (uint64_t)a2 * r.s2 +
+                  (uint64_t)a3 * r.s1;
+    uint64_t d1 = (d0 >> 32) + (uint64_t)a0 * r.r1 + (uint64_t)a1 * r.r0 +
+                  (uint64_t)a2 * r.s3 + (uint64_t)a3 * r.s2 + (uint64_t)a4 * r.s1;
+    uint64_t d2 = (d1 >> 32) + (uint64_t)a0 * r.r2 + (uint64_t)a1 * r.r1 +
+                  (uint64_t)a2 * r.r0 + (uint64_t)a3 * r.s3 + (uint64_t)a4 * r.s2;
+    uint64_t d3 = (d2 >> 32) + (uint64_t)a0 * r.r3 + (uint64_t)a1 * r.r2 +
+                  (uint64_t)a2 * r.r1 + (uint64_t)a3 * r.r0 + (uint64_t)a4 * r.s3;
+    const uint32_t h4 = a4 * r.r0 + (uint32_t)(d3 >> 32);   /* < 2^31.4 */
+    const uint32_t c = (h4 & ~3u) + (h4 >> 2);                /* 5 * (h4 >> 2) */
+    t = (uint64_t)(uint32_t)d0 + c;
+    h.h0 = (uint32_t)t;
+    t = (uint64_t)(uint32_t)d1 + (t >> 32);
+    h.h1 = (uint32_t)t;
+    t = (uint64_t)(uint32_t)d2 + (t >> 32);
+    h.h2 = (uint32_t)t;
+    t = (uint64_t)(uint32_t)d3 + (t >> 32);
+    h.h3 = (uint32_t)t;
+    h.h4 = (h4 & 3u) + (uint32_t)(t >> 32);
+}
+
+/* radix 2^32 -> five 26-bit limbs (for the rare generic multiplies) */
+NA_DEV Fe p32_to_fe(const P32 &h)
+{
+    return Fe{h.h0 & M26,
+              __builtin_amdgcn_alignbit(h.h1, h.h0, 26) & M26,
+              __builtin_amdgcn_alignbit(h.h2, h.h1, 20) & M26,
+              __builtin_amdgcn_alignbit(h.h3, h.h2, 14) & M26,
+              (h.h3 >> 8) | (h.h4 << 24)};
+}
+
+/* r^e for a wave-uniform exponent e (square-and-multiply, MSB first). */
+NA_DEV Fe fe_pow_uniform(const Fe &r, uint32_t e)
+{
+    Fe acc = Fe{1, 0, 0, 0, 0};
+    if (e == 0) return acc;
+    const Mul mr = mk_mul(r);
+    int bit = 31 - __builtin_clz(e);
+    acc = r;
+    for (--bit; bit >= 0; --bit) {
+        acc = fe_mul(acc, mk_mul(acc));
+        if ((e >> bit) & 1u) acc = fe_mul(acc, mr);
+    }
+    return acc;
 }
 
 /* ------------------------------------------------------------ record I/O */

@@ -9,40 +9,184 @@
  * bit for bit: IV = LE64(n), counter 0 -> Poly1305 key, data counters 1..;
  * Poly input = AD || pad16 || CT || pad16 || LE64(|AD|) || LE64(|CT|).
  *
- * Work decomposition (one "group" of K lanes per record, K | 64):
- *   The record's ChaCha blocks are numbered v = 0 (Poly key) .. J (J = ceil(len/64)
- *   data "units" of 64 B).  Blocks are dealt round-robin to the K lanes, aligned so
- *   that the LAST block lands on lane K-1 (slot t = v + o, lane t % K, step t / K,
- *   o = leading empty slots).  The ChaCha counter of block v is v itself.
- *   Each lane Horner-evaluates Poly1305 over the 16-B blocks of its own units:
- *   inside a unit the multiplier is r, between two of its units r^(4K-3) (the
- *   4(K-1) blocks of the other lanes sit in between).  The lane holding unit 0
- *   first absorbs the AD blocks; lane K-1 finally absorbs the length block.
- *   Lane k < K-1 then scales by r^(4(K-1-k)+q-2) (q = Poly blocks in the last
- *   unit), lane K-1 by r, and the group sums its K partial values: the result
- *   is exactly sum_i b_i r^(n-i) mod 2^130-5, the donna Horner value.
+ * A record's ChaCha blocks are v = 0 (the Poly1305 key block) .. J, J =
+ * ceil(len/64); block v >= 1 is data "unit" v-1 (64 bytes, the last one
+ * partial).  The ChaCha counter of block v is v itself.  A group of K lanes
+ * (K | 64) owns one record; two decompositions:
  *
- * Decrypt verifies first (Poly over the ciphertext), then decrypts; a record
- * whose tag fails writes nothing (cipher-chachapoly.c:139-141).  The ciphertext
- * is read twice; the second read is served by L2.
+ *  contiguous (K = 1, 2): block v goes to lane v / P, P = ceil((J+1)/K).
+ *    Each lane's Poly1305 run is a plain Horner chain with the clamped r, in
+ *    radix 2^32 (p32_block, 20 v_mad_u64_u32 per 16 B).  Lane 0 absorbs the
+ *    AD first, the lane with the last unit absorbs the length block; with
+ *    K = 2 lane 0's value is scaled by r^A (A = Poly blocks after its run).
+ *
+ *  interleaved (K = 4, 8): blocks are dealt round-robin, end-aligned so the
+ *    last block lands on lane K-1 (slot t = v + o, lane t % K, step t / K).
+ *    Each lane runs Horner in radix 2^26: multiplier r inside a unit,
+ *    r^(4K-3) between two of its units; the lane with unit 0 absorbs the AD,
+ *    lane K-1 the length block; lane k < K-1 is scaled by r^(4(K-1-k)+q-2)
+ *    (q = Poly blocks of the last unit), lane K-1 by r, then the group sums.
+ *  Both give exactly sum_i b_i r^(n-i) mod 2^130-5, the donna Horner value.
+ *
+ * Memory: a lane loads the unit of its NEXT step before running the ChaCha
+ * block of the current one.  FAST layouts (16-B aligned record slots whose
+ * input may be read up to roundup64(len)) use straight-line dwordx4 traffic
+ * in the loop; only the record's last unit and the tag take an exact-size
+ * path, after the loop.  The generic path accepts any alignment.
+ *
+ * Decrypt verifies first, then decrypts; a record whose tag fails writes
+ * nothing (cipher-chachapoly.c:139-141).  The ciphertext is read twice; the
+ * second read is served by L2.
  */
 #include "aead_device.h"
 #include "aead_kernels.h"
 
 namespace na {
 
+/* One record as seen by its group of lanes. */
+struct RecView {
+    const uint8_t *src;
+    uint8_t *dst;
+    const uint8_t *ad;
+    const uint8_t *key;   /* 32-B raw key */
+    uint64_t nonce;
+    uint32_t len, ad_len;
+};
+
+NA_DEV void load_key(const uint8_t *kp8, uint32_t key[8])
+{
+    const uint4 *kp = (const uint4 *)kp8;
+    uint4 k0 = kp[0], k1 = kp[1];
+    key[0] = k0.x; key[1] = k0.y; key[2] = k0.z; key[3] = k0.w;
+    key[4] = k1.x; key[5] = k1.y; key[6] = k1.z; key[7] = k1.w;
+}
+
+/* ------------------------------------------------------------ record I/O */
+
+/* Unit j of a record: FAST = four dwordx4 (bytes past len are garbage and
+   are masked by the caller); generic = exact bytes, zero-filled. */
+template <bool FAST>
+NA_DEV void unit_in(const uint8_t *rec, uint32_t j, uint32_t len, uint32_t w[16])
+{
+    if constexpr (FAST) {
+        const uint4 *q = (const uint4 *)(rec + 64 * j);
+        const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+        w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+        w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w;
+        w[12] = d.x; w[13] = d.y; w[14] = d.z; w[15] = d.w;
+    } else {
+        const uint32_t nb = len - 64 * j;
+        load_unit(rec + 64 * j, nb >= 64 ? 64u : nb, w);
+    }
+}
+
+/* Prefetch of unit j when `ok`.  FAST loads unconditionally (unit 0 when not
+   ok: FAST slots are readable up to roundup64(max(len,1))), so no branch
+   join forces hipcc to wait for the data right after issuing the loads. */
+template <bool FAST>
+NA_DEV void unit_prefetch(const uint8_t *rec, bool ok, uint32_t j, uint32_t len, uint32_t w[16])
+{
+    if constexpr (FAST) {
+        unit_in<true>(rec, ok ? j : 0u, len, w);
+    } else {
+        if (ok) unit_in<false>(rec, j, len, w);
+    }
+}
+
+template <bool FAST>
+NA_DEV void unit_out_full(uint8_t *p, const uint32_t w[16])
+{
+    if constexpr (FAST) {
+        uint4 *q = (uint4 *)p;
+        q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+        q[2] = make_uint4(w[8], w[9], w[10], w[11]);
+        q[3] = make_uint4(w[12], w[13], w[14], w[15]);
+    } else {
+        store_unit(p, 64, w);
+    }
+}
+
+/* the 16-B chunk c (0..3, runtime) of a unit, without dynamic indexing */
+NA_DEV void pick_chunk(const uint32_t w[16], uint32_t c, uint32_t o[4])
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        o[i] = c == 0 ? w[i] : (c == 1 ? w[4 + i] : (c == 2 ? w[8 + i] : w[12 + i]));
+}
+
+/* Exact-size store of the last unit's bytes [64(J-1), len), then (seal) the
+   tag at len.  FAST: aligned chunks as dwordx4, the partial chunk merged with
+   the tag into 8-B stores when len % 8 == 0. */
+template <bool FAST, bool TAG>
+NA_DEV void tail_out(uint8_t *rec, uint32_t J, uint32_t len, const uint32_t w[16],
+                     const uint32_t tag[4])
+{
+    if constexpr (FAST) {
+        uint32_t rem = 0, part[4] = {0, 0, 0, 0};
+        if (J >= 1) {
+            const uint32_t base = 64 * (J - 1), nb = len - base;
+#pragma unroll
+            for (uint32_t c = 0; c < 4; ++c)
+                if (16 * c + 16 <= nb)
+                    *(uint4 *)(rec + base + 16 * c) =
+                        make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+            rem = nb & 15;
+            if (rem) pick_chunk(w, nb >> 4, part);
+        }
+        const uint32_t pstart = len - rem;
+        if (rem == 8) {
+            *(uint2 *)(rec + pstart) = make_uint2(part[0], part[1]);
+            if (TAG) {
+                *(uint2 *)(rec + len) = make_uint2(tag[0], tag[1]);
+                *(uint2 *)(rec + len + 8) = make_uint2(tag[2], tag[3]);
+            }
+        } else {
+            if (rem) store16(rec + pstart, rem, part);
+            if (TAG) store16(rec + len, 16, tag);
+        }
+    } else {
+        if (J >= 1) store_unit(rec + 64 * (J - 1), len - 64 * (J - 1), w);
+        if (TAG) store16(rec + len, 16, tag);
+    }
+}
+
+template <bool FAST>
+NA_DEV void tag_in(const uint8_t *rec, uint32_t len, uint32_t t[4])
+{
+    if constexpr (FAST) {
+        if ((len & 15) == 0) {
+            const uint4 v = *(const uint4 *)(rec + len);
+            t[0] = v.x; t[1] = v.y; t[2] = v.z; t[3] = v.w;
+            return;
+        }
+        if ((len & 7) == 0) {
+            const uint2 a = *(const uint2 *)(rec + len), b = *(const uint2 *)(rec + len + 8);
+            t[0] = a.x; t[1] = a.y; t[2] = b.x; t[3] = b.y;
+            return;
+        }
+    }
+    load16(rec + len, 16, t);
+}
+
+NA_DEV bool tag_equal(const uint32_t a[4], const uint32_t b[4])
+{
+    /* constant-time, as noise_is_equal (src/protocol/util.c:188-200) */
+    return ((a[0] ^ b[0]) | (a[1] ^ b[1]) | (a[2] ^ b[2]) | (a[3] ^ b[3])) == 0;
+}
+
+/* ------------------------------------------------- interleaved (K = 4, 8) */
+
 template <int K>
 struct GroupCtx {
-    uint32_t rec;      /* record index */
-    int k;             /* lane within group */
     uint32_t J, steps, o, q;
 };
 
 template <int K>
-NA_DEV GroupCtx<K> group_ctx(uint32_t rec, int k, uint32_t len)
+NA_DEV GroupCtx<K> group_ctx(uint32_t len)
 {
     GroupCtx<K> g;
-    g.rec = rec; g.k = k;
     g.J = (len + 63) / 64;
     const uint32_t nblk = g.J + 1;
     g.steps = (nblk + K - 1) / K;
@@ -62,55 +206,42 @@ NA_DEV void poly_key_bcast(const uint32_t x[16], int src_lane, Fe &r, uint32_t s
     s[0] = kw[4]; s[1] = kw[5]; s[2] = kw[6]; s[3] = kw[7];
 }
 
-/* Powers the lane needs: the inter-unit jump r^(4K-3) and the final scale. */
+/* The inter-unit jump r^(4K-3) and the final scale of lane k. */
 template <int K>
 NA_DEV void poly_powers(const Fe &r, int k, uint32_t q, Mul &mjump, Mul &mfinal)
 {
     const Mul mr = mk_mul(r);
-    if constexpr (K == 1) {
-        mjump = mr;
-        mfinal = mr;
-        return;
-    } else {
-        const Fe r2 = fe_mul(r, mr);
-        const Mul m2 = mk_mul(r2);
-        const Fe r4 = fe_mul(r2, m2);
-        const Mul m4 = mk_mul(r4);
-        /* Q = r^(q+2), q in 1..4 */
-        const Fe qa = (q >= 3) ? r4 : r2;
-        const Mul qb = (q & 1) ? mr : m2;
-        Fe Q = fe_mul(qa, qb);
-        if (q == 2) Q = r4;
-        Fe jump;
-        Fe fin = Q;
-        const int d = K - 2 - k; /* (r^4)^d scales lane k < K-1 */
-        if constexpr (K == 2) {
-            jump = fe_mul(r4, mr); /* r^5 */
-        } else {
-            const Fe r8 = fe_mul(r4, m4);
-            const Mul m8 = mk_mul(r8);
-            if constexpr (K == 4) {
-                jump = fe_mul(fe_mul(r8, m4), mr); /* r^13 */
-                const Fe one = Fe{1, 0, 0, 0, 0};
-                const Fe sc = d == 2 ? r8 : (d == 1 ? r4 : one);
-                fin = fe_mul(Q, sc);
-            } else { /* K == 8 */
-                const Fe r16 = fe_mul(r8, m8);
-                const Mul m16 = mk_mul(r16);
-                jump = fe_mul(fe_mul(fe_mul(r16, m8), m4), mr); /* r^29 */
-                const Fe one = Fe{1, 0, 0, 0, 0};
-                Fe sc = (d & 1) ? r4 : one;
-                sc = fe_mul(sc, (d & 2) ? m8 : mk_mul(one));
-                sc = fe_mul(sc, (d & 4) ? m16 : mk_mul(one));
-                fin = fe_mul(Q, sc);
-            }
-        }
-        mjump = mk_mul(jump);
-        mfinal = (k == K - 1) ? mr : mk_mul(fin);
+    const Fe r2 = fe_mul(r, mr);
+    const Mul m2 = mk_mul(r2);
+    const Fe r4 = fe_mul(r2, m2);
+    const Mul m4 = mk_mul(r4);
+    /* Q = r^(q+2), q in 1..4 */
+    const Fe qa = (q >= 3) ? r4 : r2;
+    const Mul qb = (q & 1) ? mr : m2;
+    Fe Q = fe_mul(qa, qb);
+    if (q == 2) Q = r4;
+    const Fe r8 = fe_mul(r4, m4);
+    const Mul m8 = mk_mul(r8);
+    const Fe one = Fe{1, 0, 0, 0, 0};
+    const int d = K - 2 - k; /* lane k < K-1 is scaled by (r^4)^d * Q */
+    Fe jump, fin;
+    if constexpr (K == 4) {
+        jump = fe_mul(fe_mul(r8, m4), mr); /* r^13 */
+        fin = fe_mul(Q, d == 2 ? r8 : (d == 1 ? r4 : one));
+    } else { /* K == 8 */
+        const Fe r16 = fe_mul(r8, m8);
+        const Mul m16 = mk_mul(r16);
+        jump = fe_mul(fe_mul(fe_mul(r16, m8), m4), mr); /* r^29 */
+        Fe sc = (d & 1) ? r4 : one;
+        sc = fe_mul(sc, (d & 2) ? m8 : mk_mul(one));
+        sc = fe_mul(sc, (d & 4) ? m16 : mk_mul(one));
+        fin = fe_mul(Q, sc);
     }
+    mjump = mk_mul(jump);
+    mfinal = (k == K - 1) ? mr : mk_mul(fin);
 }
 
-/* Horner over AD (lane holding unit 0 only): acc = acc*r + block, padded. */
+/* Horner over AD (radix 2^26): acc = acc*r + block, zero-padded. */
 NA_DEV void poly_ad(Fe &acc, const Mul &mr, const uint8_t *ad, uint32_t ad_len)
 {
     for (uint32_t off = 0; off < ad_len; off += 16) {
@@ -122,10 +253,10 @@ NA_DEV void poly_ad(Fe &acc, const Mul &mr, const uint8_t *ad, uint32_t ad_len)
     }
 }
 
-/* Horner over one 64-B unit of ciphertext (nb Poly blocks, 1..4). */
-NA_DEV void poly_unit(Fe &acc, const Mul &mjump, const Mul &mr, const uint32_t c[16], uint32_t nb)
+/* Horner over one unit of ciphertext (nb Poly blocks, 1..4). */
+NA_DEV void poly_unit(Fe &acc, const Mul &mfirst, const Mul &mr, const uint32_t c[16], uint32_t nb)
 {
-    acc = fe_mul(acc, mjump);
+    acc = fe_mul(acc, mfirst);
     fe_add_block(acc, c[0], c[1], c[2], c[3]);
 #pragma unroll
     for (uint32_t b = 1; b < 4; ++b) {
@@ -136,7 +267,7 @@ NA_DEV void poly_unit(Fe &acc, const Mul &mjump, const Mul &mr, const uint32_t c
     }
 }
 
-/* Close the group's Poly1305: length block, scale, group sum, + s. */
+/* Length block on lane K-1, scale, group sum, + s. */
 template <int K>
 NA_DEV void poly_close(Fe acc, int k, const Mul &mr, const Mul &mfinal, uint64_t ad_len,
                        uint64_t len, const uint32_t s[4], uint32_t tag[4])
@@ -151,44 +282,33 @@ NA_DEV void poly_close(Fe acc, int k, const Mul &mr, const Mul &mfinal, uint64_t
     fe_finish(acc, s, tag);
 }
 
-/* One record as seen by its group of K lanes. */
-struct RecView {
-    const uint8_t *src;
-    uint8_t *dst;
-    const uint8_t *ad;
-    const uint8_t *key;   /* 32-B raw key */
-    uint64_t nonce;
-    uint32_t len, ad_len;
-};
-
-NA_DEV void load_key(const uint8_t *kp8, uint32_t key[8])
-{
-    const uint4 *kp = (const uint4 *)kp8;
-    uint4 k0 = kp[0], k1 = kp[1];
-    key[0] = k0.x; key[1] = k0.y; key[2] = k0.z; key[3] = k0.w;
-    key[4] = k1.x; key[5] = k1.y; key[6] = k1.z; key[7] = k1.w;
-}
-
-/* ------------------------------------------------------------- encrypt */
-
-template <int K>
-NA_DEV void seal_record(const RecView &rv, int k)
+template <int K, bool FAST>
+NA_DEV void seal_il(const RecView &rv, int k)
 {
     uint32_t key[8];
     load_key(rv.key, key);
-    const uint64_t nonce = rv.nonce;
+    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
     const uint32_t len = rv.len;
-    const GroupCtx<K> g = group_ctx<K>(0, k, len);
-    const int lane = (int)(threadIdx.x & 63);
-    const int gbase = lane & ~(K - 1);
+    const GroupCtx<K> g = group_ctx<K>(len);
+    const int gbase = (int)(threadIdx.x & 63) & ~(K - 1);
 
     Fe acc = fe_zero(), r;
     Mul mr, mjump, mfinal;
-    uint32_t s[4];
+    uint32_t s[4], wn[16], wc[16], x[16];
+    bool seen = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wn[i] = 0;
+    {
+        const int v = k - (int)g.o;
+        unit_prefetch<FAST>(rv.src, v >= 1, (uint32_t)v - 1, len, wn);
+    }
     for (uint32_t m = 0; m < g.steps; ++m) {
         const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
-        uint32_t x[16];
-        chacha20_block(key, (uint32_t)v, 0u, (uint32_t)nonce, (uint32_t)(nonce >> 32), x);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wc[i] = wn[i];
+        const int vn = v + K; /* the unit of the next step, loaded now */
+        unit_prefetch<FAST>(rv.src, m + 1 < g.steps && vn >= 1, (uint32_t)vn - 1, len, wn);
+        chacha20_block(key, (uint32_t)v, 0u, n_lo, n_hi, x);
         if (m == 0) {
             poly_key_bcast(x, gbase + (int)g.o, r, s);
             mr = mk_mul(r);
@@ -197,45 +317,45 @@ NA_DEV void seal_record(const RecView &rv, int k)
             const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
             if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
         }
-        if (v >= 1) {
-            const uint32_t j = (uint32_t)v - 1;
-            const uint32_t nbytes = (j + 1 < g.J) ? 64u : len - 64 * j;
+        if (v >= 1 && (uint32_t)v < g.J) { /* a full unit */
             uint32_t w[16];
-            load_unit(rv.src + 64 * j, nbytes, w);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-            mask_unit(w, nbytes);
-            store_unit(rv.dst + 64 * j, nbytes, w);
-            /* A lane's first unit follows the AD directly (exponent gap 1) or
-               starts from acc = 0, where any multiplier works: use r. */
-            const bool first = (m == 0) || (m == 1 && k <= (int)g.o);
-            poly_unit(acc, first ? mr : mjump, mr, w, (nbytes + 15) / 16);
+            for (int i = 0; i < 16; ++i) w[i] = wc[i] ^ x[i];
+            unit_out_full<FAST>(rv.dst + 64 * (v - 1), w);
+            /* a lane's first unit follows the AD directly (gap 1) or starts
+               from acc = 0, where any multiplier works: use r */
+            poly_unit(acc, seen ? mjump : mr, mr, w, 4);
+            seen = true;
         }
+    }
+    /* the last unit (block J) is lane K-1's last step */
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = wc[i] ^ x[i];
+    if (k == K - 1 && g.J >= 1) {
+        const uint32_t nb = len - 64 * (g.J - 1);
+        mask_unit(w, nb);
+        poly_unit(acc, seen ? mjump : mr, mr, w, (nb + 15) / 16);
     }
     uint32_t tag[4];
     poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
-    if (k == K - 1) store16(rv.dst + len, 16, tag);
+    if (k == K - 1) tail_out<FAST, true>(rv.dst, g.J, len, w, tag);
 }
 
-/* ------------------------------------------------------------- decrypt */
-
-/* Returns true when the tag verified (identical on every lane of the group). */
-template <int K>
-NA_DEV bool open_record(const RecView &rv, int k)
+template <int K, bool FAST>
+NA_DEV bool open_il(const RecView &rv, int k)
 {
     uint32_t key[8];
     load_key(rv.key, key);
-    const uint64_t nonce = rv.nonce;
+    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
     const uint32_t len = rv.len;
-    const GroupCtx<K> g = group_ctx<K>(0, k, len);
-    const int lane = (int)(threadIdx.x & 63);
-    const int gbase = lane & ~(K - 1);
+    const GroupCtx<K> g = group_ctx<K>(len);
+    const int gbase = (int)(threadIdx.x & 63) & ~(K - 1);
 
-    /* step-0 key stream: block 0 on lane o (Poly key), data on the others —
-       kept in registers for the decrypt phase */
+    /* step-0 key stream: block 0 on lane o, data on the others (kept) */
     const int v0 = k - (int)g.o;
     uint32_t x0[16];
-    chacha20_block(key, (uint32_t)v0, 0u, (uint32_t)nonce, (uint32_t)(nonce >> 32), x0);
+    chacha20_block(key, (uint32_t)v0, 0u, n_lo, n_hi, x0);
     Fe r;
     uint32_t s[4];
     poly_key_bcast(x0, gbase + (int)g.o, r, s);
@@ -247,47 +367,534 @@ NA_DEV bool open_record(const RecView &rv, int k)
     if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
 
     /* phase 1: authenticate the ciphertext */
+    uint32_t wn[16], wc[16];
+    bool seen = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wn[i] = 0;
+    unit_prefetch<FAST>(rv.src, v0 >= 1, (uint32_t)v0 - 1, len, wn);
     for (uint32_t m = 0; m < g.steps; ++m) {
         const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wc[i] = wn[i];
+        const int vn = v + K;
+        unit_prefetch<FAST>(rv.src, m + 1 < g.steps && vn >= 1, (uint32_t)vn - 1, len, wn);
         if (v >= 1) {
             const uint32_t j = (uint32_t)v - 1;
-            const uint32_t nbytes = (j + 1 < g.J) ? 64u : len - 64 * j;
-            uint32_t w[16];
-            load_unit(rv.src + 64 * j, nbytes, w);
-            const bool first = (m == 0) || (m == 1 && k <= (int)g.o);
-            poly_unit(acc, first ? mr : mjump, mr, w, (nbytes + 15) / 16);
+            uint32_t nb = 4;
+            if (j + 1 == g.J) {
+                const uint32_t bytes = len - 64 * j;
+                mask_unit(wc, bytes);
+                nb = (bytes + 15) / 16;
+            }
+            poly_unit(acc, seen ? mjump : mr, mr, wc, nb);
+            seen = true;
         }
     }
     uint32_t tag[4], got[4];
     poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
-    load16(rv.src + len, 16, got);
-    const uint32_t diff = (tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3]);
-    if (diff != 0) return false; /* noise_is_equal, util.c:188-200: nothing written */
+    tag_in<FAST>(rv.src, len, got);
+    if (!tag_equal(tag, got)) return false; /* identical verdict on the group */
 
     /* phase 2: decrypt (the ciphertext re-read is served by L2) */
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wn[i] = 0;
+    unit_prefetch<FAST>(rv.src, v0 >= 1, (uint32_t)v0 - 1, len, wn);
+    uint32_t x[16];
     for (uint32_t m = 0; m < g.steps; ++m) {
         const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
-        if (v >= 1) {
-            uint32_t x[16];
-            if (m == 0) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) x[i] = x0[i];
-            } else {
-                chacha20_block(key, (uint32_t)v, 0u, (uint32_t)nonce, (uint32_t)(nonce >> 32), x);
-            }
-            const uint32_t j = (uint32_t)v - 1;
-            const uint32_t nbytes = (j + 1 < g.J) ? 64u : len - 64 * j;
-            uint32_t w[16];
-            load_unit(rv.src + 64 * j, nbytes, w);
+        for (int i = 0; i < 16; ++i) wc[i] = wn[i];
+        const int vn = v + K;
+        unit_prefetch<FAST>(rv.src, m + 1 < g.steps && vn >= 1, (uint32_t)vn - 1, len, wn);
+        if (m == 0) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-            store_unit(rv.dst + 64 * j, nbytes, w);
+            for (int i = 0; i < 16; ++i) x[i] = x0[i];
+        } else {
+            chacha20_block(key, (uint32_t)v, 0u, n_lo, n_hi, x);
         }
+        if (v >= 1 && (uint32_t)v < g.J) {
+            uint32_t w[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = wc[i] ^ x[i];
+            unit_out_full<FAST>(rv.dst + 64 * (v - 1), w);
+        }
+    }
+    if (k == K - 1 && g.J >= 1) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = wc[i] ^ x[i];
+        tail_out<FAST, false>(rv.dst, g.J, len, w, nullptr);
+    }
+    return true;
+}
+
+/* --------------------------- interleaved, LDS-staged (uniform FAST batches)
+ *
+ * Same decomposition as seal_il/open_il, but the wave's global traffic is
+ * re-shaped through a 4 KB LDS tile.  At every step lane L of the wave owns
+ * one unit (unit j0 + L%K of record rec0 + L/K).  Coalesced wave-instruction
+ * i (0..3), lane l moves chunk c = l%4 of the unit owned by L = 16i + l/4, so
+ * one instruction covers the 256-B (K=4) or 512-B (K=8) contiguous runs of
+ * whole records: full 128-B lines instead of 64 scattered 16-B pieces.  The
+ * tile slot of (L, c) is L*4 + (c ^ ((L>>2)&3)) (uint4 units): the XOR makes
+ * both the owner-side and the coalesced-side ds_*_b128 bank-conflict-free.
+ * Every lane of the wave takes part in every exchange (no early exit); lanes
+ * past the batch end are clamped onto the last record and store nothing.
+ */
+
+NA_DEV RecView uniform_view(const UniformArgs &a, uint32_t rec);
+
+NA_DEV uint32_t tile_slot(uint32_t L, uint32_t c) { return L * 4 + (c ^ ((L >> 2) & 3)); }
+
+NA_DEV void tile_get_unit(const uint4 *t, uint32_t L, uint32_t w[16])
+{
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) {
+        const uint4 v = t[tile_slot(L, c)];
+        w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+    }
+}
+
+/* four coalesced 16-B pieces, held by value (an array here gets demoted to
+   scratch by hipcc once it is live across the ChaCha block) */
+struct Quad { uint4 a, b, c, d; };
+
+NA_DEV void tile_put_coalesced(uint4 *t, uint32_t lane, const Quad &P)
+{
+    const uint32_t q = lane >> 2, c = lane & 3;
+    t[tile_slot(q, c)] = P.a;
+    t[tile_slot(16u + q, c)] = P.b;
+    t[tile_slot(32u + q, c)] = P.c;
+    t[tile_slot(48u + q, c)] = P.d;
+}
+
+NA_DEV void tile_put_unit(uint4 *t, uint32_t L, const uint32_t w[16])
+{
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c)
+        t[tile_slot(L, c)] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+}
+
+/* The wave's coalesced view: for instruction i, this lane serves owner
+   L = 16i + lane/4 — record rec0 + L/K, unit offset L%K, chunk lane%4. */
+template <int K>
+struct WaveIO {
+    const uint8_t *in[4];
+    uint8_t *out[4];
+    uint32_t kk[4];
+    bool live[4];
+};
+
+template <int K>
+NA_DEV WaveIO<K> wave_io(const UniformArgs &a, uint32_t rec0, uint32_t lane)
+{
+    WaveIO<K> io;
+    const uint32_t c = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t L = 16u * i + (lane >> 2);
+        const uint32_t r = rec0 + L / K;
+        io.live[i] = r < a.n_records;
+        const uint32_t rc = io.live[i] ? r : a.n_records - 1;
+        io.in[i] = a.in + (size_t)rc * a.in_stride + 16 * c;
+        io.out[i] = a.out + (size_t)rc * a.out_stride + 16 * c;
+        io.kk[i] = L % K;
+    }
+    return io;
+}
+
+/* Coalesced loads of step unit base j0 (unit of owner offset kk = j0 + kk,
+   clamped to unit 0 where it does not exist). */
+template <int K>
+NA_DEV Quad wave_load(const WaveIO<K> &io, int j0)
+{
+    int u0 = j0 + (int)io.kk[0], u1 = j0 + (int)io.kk[1];
+    int u2 = j0 + (int)io.kk[2], u3 = j0 + (int)io.kk[3];
+    Quad P;
+    P.a = *(const uint4 *)(io.in[0] + 64 * (u0 > 0 ? u0 : 0));
+    P.b = *(const uint4 *)(io.in[1] + 64 * (u1 > 0 ? u1 : 0));
+    P.c = *(const uint4 *)(io.in[2] + 64 * (u2 > 0 ? u2 : 0));
+    P.d = *(const uint4 *)(io.in[3] + 64 * (u3 > 0 ? u3 : 0));
+    return P;
+}
+
+template <int K>
+NA_DEV void wave_store(const WaveIO<K> &io, int j0, int last_full, const uint4 *t, uint32_t lane,
+                       const bool okL[4])
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 q = t[tile_slot(16u * i + (lane >> 2), lane & 3)];
+        const int u = j0 + (int)io.kk[i];
+        if (io.live[i] && okL[i] && u >= 0 && u <= last_full) *(uint4 *)(io.out[i] + 64 * u) = q;
+    }
+}
+
+template <int K>
+NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tile)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t rec0 = ((blockIdx.x * 256u + threadIdx.x) >> 6) * (64 / K);
+    const uint32_t rec_raw = rec0 + lane / K;
+    const bool live = rec_raw < a.n_records;
+    const RecView rv = uniform_view(a, live ? rec_raw : a.n_records - 1);
+    const int k = (int)(lane % K);
+    uint32_t key[8];
+    load_key(rv.key, key);
+    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
+    const uint32_t len = rv.len;
+    const GroupCtx<K> g = group_ctx<K>(len);
+    const int gbase = (int)lane & ~(K - 1);
+    const WaveIO<K> io = wave_io<K>(a, rec0, lane);
+    const bool all_ok[4] = {true, true, true, true};
+    const int last_full = (int)g.J - 2; /* unit J-1 is the tail, stored after */
+
+    Fe acc = fe_zero(), r;
+    Mul mr, mjump, mfinal;
+    uint32_t s[4], x[16], wt[16];
+    bool seen = false;
+    Quad P = wave_load<K>(io, -(int)g.o - 1);
+    tile_put_coalesced(tile, lane, P);
+    for (uint32_t m = 0; m < g.steps; ++m) {
+        const int j0 = (int)(m * K) - (int)g.o - 1;
+        const int v = j0 + 1 + k;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t w[16];
+        tile_get_unit(tile, lane, w);
+        __builtin_amdgcn_wave_barrier();
+        /* next step's bytes: issued now, parked in the tile at the end of
+           this iteration — no loop-carried load registers, so hipcc's wait
+           lands after the ChaCha block instead of right after the loads */
+        const bool more = m + 1 < g.steps;
+        P = wave_load<K>(io, more ? j0 + K : j0);
+        chacha20_block(key, (uint32_t)v, 0u, n_lo, n_hi, x);
+        if (m == 0) {
+            poly_key_bcast(x, gbase + (int)g.o, r, s);
+            mr = mk_mul(r);
+            poly_powers<K>(r, k, g.q, mjump, mfinal);
+            const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
+            if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+        if (v >= 1 && (uint32_t)v < g.J) {
+            poly_unit(acc, seen ? mjump : mr, mr, w, 4);
+            seen = true;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wt[i] = w[i];
+        tile_put_unit(tile, lane, w);
+        __builtin_amdgcn_wave_barrier();
+        wave_store<K>(io, j0, last_full, tile, lane, all_ok);
+        __builtin_amdgcn_wave_barrier();
+        tile_put_coalesced(tile, lane, P); /* harmless after the last step */
+    }
+    /* the last unit (block J) is lane K-1's last step */
+    if (k == K - 1 && g.J >= 1) {
+        const uint32_t nb = len - 64 * (g.J - 1);
+        mask_unit(wt, nb);
+        poly_unit(acc, seen ? mjump : mr, mr, wt, (nb + 15) / 16);
+    }
+    uint32_t tag[4];
+    poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
+    if (k == K - 1 && live) tail_out<true, true>(rv.dst, g.J, len, wt, tag);
+}
+
+template <int K>
+NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tile)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t rec0 = ((blockIdx.x * 256u + threadIdx.x) >> 6) * (64 / K);
+    const uint32_t rec_raw = rec0 + lane / K;
+    const bool live = rec_raw < a.n_records;
+    const RecView rv = uniform_view(a, live ? rec_raw : a.n_records - 1);
+    const int k = (int)(lane % K);
+    uint32_t key[8];
+    load_key(rv.key, key);
+    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
+    const uint32_t len = rv.len;
+    const GroupCtx<K> g = group_ctx<K>(len);
+    const int gbase = (int)lane & ~(K - 1);
+    const WaveIO<K> io = wave_io<K>(a, rec0, lane);
+    const int last_full = (int)g.J - 2;
+
+    const int v0 = k - (int)g.o;
+    uint32_t x0[16];
+    chacha20_block(key, (uint32_t)v0, 0u, n_lo, n_hi, x0);
+    Fe r;
+    uint32_t s[4];
+    poly_key_bcast(x0, gbase + (int)g.o, r, s);
+    const Mul mr = mk_mul(r);
+    Mul mjump, mfinal;
+    poly_powers<K>(r, k, g.q, mjump, mfinal);
+    Fe acc = fe_zero();
+    const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
+    if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
+
+    /* phase 1: authenticate */
+    bool seen = false;
+    Quad P = wave_load<K>(io, -(int)g.o - 1);
+    tile_put_coalesced(tile, lane, P);
+    for (uint32_t m = 0; m < g.steps; ++m) {
+        const int j0 = (int)(m * K) - (int)g.o - 1;
+        const int v = j0 + 1 + k;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t w[16];
+        tile_get_unit(tile, lane, w);
+        __builtin_amdgcn_wave_barrier();
+        const bool more = m + 1 < g.steps;
+        P = wave_load<K>(io, more ? j0 + K : j0);
+        if (v >= 1) {
+            uint32_t nb = 4;
+            if ((uint32_t)v == g.J) {
+                const uint32_t bytes = len - 64 * (g.J - 1);
+                mask_unit(w, bytes);
+                nb = (bytes + 15) / 16;
+            }
+            poly_unit(acc, seen ? mjump : mr, mr, w, nb);
+            seen = true;
+        }
+        __builtin_amdgcn_wave_barrier();
+        tile_put_coalesced(tile, lane, P); /* harmless after the last step */
+    }
+    uint32_t tag[4], got[4];
+    poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
+    tag_in<true>(rv.src, len, got);
+    const bool ok = tag_equal(tag, got);
+    if (k == K - 1 && live && a.status) a.status[rec_raw] = ok ? 0 : 1;
+    /* verdict of the owner each coalesced slot serves */
+    bool okL[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) okL[i] = __shfl((int)ok, (int)(16u * i + (lane >> 2)), 64) != 0;
+
+    /* phase 2: decrypt (wave-uniform: every lane joins the exchanges) */
+    uint32_t x[16], wt[16];
+    P = wave_load<K>(io, -(int)g.o - 1);
+    tile_put_coalesced(tile, lane, P);
+    for (uint32_t m = 0; m < g.steps; ++m) {
+        const int j0 = (int)(m * K) - (int)g.o - 1;
+        const int v = j0 + 1 + k;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t w[16];
+        tile_get_unit(tile, lane, w);
+        __builtin_amdgcn_wave_barrier();
+        const bool more = m + 1 < g.steps;
+        P = wave_load<K>(io, more ? j0 + K : j0);
+        if (m == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = x0[i];
+        } else {
+            chacha20_block(key, (uint32_t)v, 0u, n_lo, n_hi, x);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wt[i] = w[i] ^ x[i];
+        tile_put_unit(tile, lane, wt);
+        __builtin_amdgcn_wave_barrier();
+        wave_store<K>(io, j0, last_full, tile, lane, okL);
+        __builtin_amdgcn_wave_barrier();
+        tile_put_coalesced(tile, lane, P); /* harmless after the last step */
+    }
+    if (k == K - 1 && live && ok && g.J >= 1) tail_out<true, false>(rv.dst, g.J, len, wt, nullptr);
+}
+
+/* ------------------------------------------------- contiguous (K = 1, 2) */
+
+NA_DEV void p32_ad(P32 &acc, const R32 &r, const uint8_t *ad, uint32_t ad_len)
+{
+    for (uint32_t off = 0; off < ad_len; off += 16) {
+        uint32_t w[4];
+        const uint32_t n = ad_len - off;
+        load16(ad + off, n >= 16 ? 16u : n, w);
+        p32_block(acc, r, w[0], w[1], w[2], w[3]);
+    }
+}
+
+NA_DEV void p32_unit(P32 &acc, const R32 &r, const uint32_t c[16], uint32_t nb)
+{
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b)
+        if (b < nb) p32_block(acc, r, c[4 * b], c[4 * b + 1], c[4 * b + 2], c[4 * b + 3]);
+}
+
+struct CtPlan {
+    uint32_t J, nblk, P, v0, v1, M;
+    bool holds_last;
+};
+
+template <int G>
+NA_DEV CtPlan ct_plan(uint32_t len, int k)
+{
+    CtPlan p;
+    p.J = (len + 63) / 64;
+    p.nblk = p.J + 1;
+    p.P = (p.nblk + G - 1) / G;
+    p.v0 = (uint32_t)k * p.P;
+    p.v1 = min(p.v0 + p.P, p.nblk);
+    p.M = (len + 15) / 16;
+    p.holds_last = p.v0 < p.nblk && p.v1 == p.nblk;
+    return p;
+}
+
+/* Length block on the last lane; with G = 2 lane 0 scaled by r^A; + s. */
+template <int G>
+NA_DEV void ct_close(P32 acc, const CtPlan &p, int k, const R32 &r, const Fe &r26,
+                     uint64_t ad_len, uint64_t len, const uint32_t s[4], uint32_t tag[4])
+{
+    if (p.holds_last)
+        p32_block(acc, r, (uint32_t)ad_len, (uint32_t)(ad_len >> 32), (uint32_t)len,
+                  (uint32_t)(len >> 32));
+    Fe a = p32_to_fe(acc);
+    if constexpr (G == 2) {
+        /* Poly blocks after lane 0's run: lane 1's units + the length block */
+        const uint32_t A = p.nblk > p.P ? p.M - 4 * (p.P - 1) + 1 : 0u;
+        const Fe rA = fe_pow_uniform(r26, A);
+        if (k == 0) a = fe_mul(a, mk_mul(rA));
+        a = fe_group_sum<2>(a);
+    }
+    fe_finish(a, s, tag);
+}
+
+template <int G>
+NA_DEV void key_words_bcast(const uint32_t x[16], int gbase, uint32_t kw[8])
+{
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kw[i] = G == 1 ? x[i] : (uint32_t)__shfl((int)x[i], gbase, 64);
+}
+
+template <int G, bool FAST>
+NA_DEV void seal_ct(const RecView &rv, int k)
+{
+    uint32_t key[8];
+    load_key(rv.key, key);
+    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
+    const uint32_t len = rv.len;
+    const CtPlan p = ct_plan<G>(len, k);
+    const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
+
+    uint32_t wn[16], wc[16], x[16], wt[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wn[i] = wt[i] = 0;
+    unit_prefetch<FAST>(rv.src, p.v0 >= 1 && p.v0 < p.v1, p.v0 - 1, len, wn);
+    P32 acc = p32_zero();
+    R32 r;
+    Fe r26;
+    uint32_t s[4];
+    for (uint32_t m = 0; m < p.P; ++m) {
+        const uint32_t v = p.v0 + m;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wc[i] = wn[i];
+        unit_prefetch<FAST>(rv.src, v + 1 < p.v1, v, len, wn); /* unit of block v+1 */
+        chacha20_block(key, v, 0u, n_lo, n_hi, x);
+        if (m == 0) {
+            uint32_t kw[8];
+            key_words_bcast<G>(x, gbase, kw);
+            r = r32_from_key(kw[0], kw[1], kw[2], kw[3]);
+            r26 = fe_clamp_r(kw[0], kw[1], kw[2], kw[3]);
+            s[0] = kw[4]; s[1] = kw[5]; s[2] = kw[6]; s[3] = kw[7];
+            if (k == 0 && rv.ad_len) p32_ad(acc, r, rv.ad, rv.ad_len);
+        }
+        if (v >= 1 && v < p.v1) {
+            uint32_t w[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = wc[i] ^ x[i];
+            if (v < p.J) {
+                unit_out_full<FAST>(rv.dst + 64 * (v - 1), w);
+                p32_unit(acc, r, w, 4);
+            } else { /* the last unit */
+                const uint32_t nb = len - 64 * (v - 1);
+                mask_unit(w, nb);
+                p32_unit(acc, r, w, (nb + 15) / 16);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) wt[i] = w[i];
+            }
+        }
+    }
+    uint32_t tag[4];
+    ct_close<G>(acc, p, k, r, r26, rv.ad_len, len, s, tag);
+    if (p.holds_last) tail_out<FAST, true>(rv.dst, p.J, len, wt, tag);
+}
+
+template <int G, bool FAST>
+NA_DEV bool open_ct(const RecView &rv, int k)
+{
+    uint32_t key[8];
+    load_key(rv.key, key);
+    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
+    const uint32_t len = rv.len;
+    const CtPlan p = ct_plan<G>(len, k);
+    const int gbase = (int)(threadIdx.x & 63) & ~(G - 1);
+
+    uint32_t x0[16];
+    chacha20_block(key, p.v0, 0u, n_lo, n_hi, x0);
+    uint32_t kw[8];
+    key_words_bcast<G>(x0, gbase, kw);
+    const R32 r = r32_from_key(kw[0], kw[1], kw[2], kw[3]);
+    const Fe r26 = fe_clamp_r(kw[0], kw[1], kw[2], kw[3]);
+    const uint32_t s[4] = {kw[4], kw[5], kw[6], kw[7]};
+    P32 acc = p32_zero();
+    if (k == 0 && rv.ad_len) p32_ad(acc, r, rv.ad, rv.ad_len);
+
+    /* phase 1: authenticate (one unit ahead) */
+    const uint32_t u0 = p.v0 >= 1 ? p.v0 : 1u; /* first block with data */
+    uint32_t wn[16], wc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wn[i] = 0;
+    unit_prefetch<FAST>(rv.src, u0 < p.v1, u0 - 1, len, wn);
+    for (uint32_t v = u0; v < p.v1; ++v) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wc[i] = wn[i];
+        unit_prefetch<FAST>(rv.src, v + 1 < p.v1, v, len, wn);
+        uint32_t nb = 4;
+        if (v == p.J) {
+            const uint32_t bytes = len - 64 * (v - 1);
+            mask_unit(wc, bytes);
+            nb = (bytes + 15) / 16;
+        }
+        p32_unit(acc, r, wc, nb);
+    }
+    uint32_t tag[4], got[4];
+    ct_close<G>(acc, p, k, r, r26, rv.ad_len, len, s, tag);
+    tag_in<FAST>(rv.src, len, got);
+    if (!tag_equal(tag, got)) return false;
+
+    /* phase 2: decrypt; the ciphertext re-read is served by L2 */
+    unit_prefetch<FAST>(rv.src, u0 < p.v1, u0 - 1, len, wn);
+    for (uint32_t v = u0; v < p.v1; ++v) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wc[i] = wn[i];
+        unit_prefetch<FAST>(rv.src, v + 1 < p.v1, v, len, wn);
+        uint32_t x[16];
+        if (v == p.v0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = x0[i];
+        } else {
+            chacha20_block(key, v, 0u, n_lo, n_hi, x);
+        }
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = wc[i] ^ x[i];
+        if (v < p.J) unit_out_full<FAST>(rv.dst + 64 * (v - 1), w);
+        else tail_out<FAST, false>(rv.dst, p.J, len, w, nullptr);
     }
     return true;
 }
 
 /* ------------------------------------------------------------- kernels */
+
+/* lanes per record: 1 or 2 -> contiguous runs, 4 or 8 -> interleaved units */
+template <int K, bool FAST>
+NA_DEV void seal_any(const RecView &rv, int k)
+{
+    if constexpr (K <= 2) seal_ct<K, FAST>(rv, k);
+    else seal_il<K, FAST>(rv, k);
+}
+
+template <int K, bool FAST>
+NA_DEV bool open_any(const RecView &rv, int k)
+{
+    if constexpr (K <= 2) return open_ct<K, FAST>(rv, k);
+    else return open_il<K, FAST>(rv, k);
+}
 
 NA_DEV RecView uniform_view(const UniformArgs &a, uint32_t rec)
 {
@@ -317,43 +924,53 @@ NA_DEV RecView ragged_view(const RaggedArgs &a, uint32_t rec)
     return rv;
 }
 
-template <int K>
+template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_seal_uniform(UniformArgs a)
 {
+    if constexpr (K >= 4 && FAST) {
+        __shared__ uint4 tiles[4][256]; /* 4 KB per wave */
+        seal_il_staged<K>(a, tiles[threadIdx.x >> 6]);
+        return;
+    }
     const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t rec = gtid / K;
     if (rec >= a.n_records) return; /* whole groups leave together (K | 64) */
-    seal_record<K>(uniform_view(a, rec), (int)(gtid % K));
+    seal_any<K, FAST>(uniform_view(a, rec), (int)(gtid % K));
 }
 
-template <int K>
+template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_open_uniform(UniformArgs a)
 {
+    if constexpr (K >= 4 && FAST) {
+        __shared__ uint4 tiles[4][256];
+        open_il_staged<K>(a, tiles[threadIdx.x >> 6]);
+        return;
+    }
     const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t rec = gtid / K;
     if (rec >= a.n_records) return;
     const int k = (int)(gtid % K);
-    const bool ok = open_record<K>(uniform_view(a, rec), k);
+    const bool ok = open_any<K, FAST>(uniform_view(a, rec), k);
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
-template <int K>
+template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_seal_ragged(RaggedArgs a)
 {
     const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t rec = gtid / K;
     if (rec >= a.n_records) return;
-    seal_record<K>(ragged_view(a, rec), (int)(gtid % K));
+    seal_any<K, FAST>(ragged_view(a, rec), (int)(gtid % K));
 }
 
-template <int K>
+template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
 {
     const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t rec = gtid / K;
     if (rec >= a.n_records) return;
     const int k = (int)(gtid % K);
-    const bool ok = open_record<K>(ragged_view(a, rec), k);
+    const bool ok = open_any<K, FAST>(ragged_view(a, rec), k);
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 

@@ -200,6 +200,14 @@ typedef struct {
 
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+/* A record's staging slot: 16-B aligned, readable up to roundup64(len) and
+   large enough for CT || tag — the NOISE_AEAD_FLAG_FAST layout. */
+static size_t slot_bytes(size_t len)
+{
+    size_t a = ((len ? len : 1) + 63) & ~(size_t)63, b = align16(len + 16);
+    return a > b ? a : b;
+}
+
 /* Run a set of jobs (any mix of states and ciphers) in one staging round
    trip: pack records into pinned memory, one H2D, one ragged kernel per
    cipher, one D2H.  Fills job.status.  Seal results are copied back at once;
@@ -214,7 +222,7 @@ static int run_jobs(Job *jobs, size_t n, int open)
     const size_t status_off = off;
     off = align16(off + n);
     const size_t payload_off = off;
-    for (size_t i = 0; i < n; ++i) off += align16(jobs[i].ad_len) + align16(jobs[i].len + 16);
+    for (size_t i = 0; i < n; ++i) off += align16(jobs[i].ad_len) + slot_bytes(jobs[i].len);
     const size_t total = off + 64;
     Staging *sg = stage_get(total);
     if (!sg) {
@@ -253,7 +261,7 @@ static int run_jobs(Job *jobs, size_t n, int open)
         p += align16(j->ad_len);
         r->in_off = r->out_off = p;
         memcpy(sg->h + p, j->data, j->len + (open ? 16 : 0));
-        p += align16(j->len + 16);
+        p += slot_bytes(j->len);
         r->len = (uint32_t)j->len;
         r->nonce = j->nonce;
         r->ctx_off = (uint64_t)(uintptr_t)j->st->d_ctx;
@@ -273,6 +281,8 @@ static int run_jobs(Job *jobs, size_t n, int open)
         job.status = sg->d + status_off + first;
         job.n_records = (uint32_t)count;
         job.lanes_per_record = 0;
+        job.flags = NOISE_AEAD_FLAG_FAST;
+        job.reserved_ = 0;
         int cid = c == 0 ? NOISE_CIPHER_CHACHAPOLY : NOISE_CIPHER_AESGCM;
         rc = open ? noise_aead_dev_open_ragged(cid, &job, stream)
                   : noise_aead_dev_seal_ragged(cid, &job, stream);

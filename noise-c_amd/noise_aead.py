@@ -71,9 +71,11 @@ class NoiseAeadRecord(C.Structure):
 class NoiseAeadRagged(C.Structure):
     _fields_ = [("ctx_base", C.c_void_p), ("recs", C.c_void_p), ("in_", C.c_void_p),
                 ("out", C.c_void_p), ("ad", C.c_void_p), ("status", C.c_void_p),
-                ("n_records", C.c_uint32), ("lanes_per_record", C.c_uint32)]
+                ("n_records", C.c_uint32), ("lanes_per_record", C.c_uint32),
+                ("flags", C.c_uint32), ("reserved_", C.c_uint32)]
 
 
+FLAG_FAST = 1
 _LIB = None
 
 
@@ -269,9 +271,9 @@ def dev_uniform(open_: bool, cipher: int, *, ctx: int, nonce_base: int, inp: int
 
 def dev_ragged(open_: bool, cipher: int, *, ctx_base: int, recs: int, inp: int, out: int,
                n_records: int, status: int = 0, ad: int = 0, lanes: int = 0,
-               stream: int = 0) -> int:
+               flags: int = 0, stream: int = 0) -> int:
     j = NoiseAeadRagged(ctx_base or None, recs, inp, out, ad or None, status or None,
-                        n_records, lanes)
+                        n_records, lanes, flags, 0)
     f = lib().noise_aead_dev_open_ragged if open_ else lib().noise_aead_dev_seal_ragged
     return f(cipher, C.byref(j), stream or None)
 

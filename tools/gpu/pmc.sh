@@ -1,0 +1,20 @@
+# PMC passes for the bench kernels (one rocprofv3 run per counter group;
+# --pmc with --kernel-trace only, as the pool requires).  Usage:
+#   bash tools/gpu/pmc.sh CONFIG OUTDIR [extra bench args]
+set -u
+R=$GRAFT_REPO_ROOT
+CFG=${1:-c2}; OUT=${2:-$R/gpurun_out/pmc_$CFG}; shift 2 || true
+EXTRA="$@"
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+run() {  # name counters...
+  local name=$1; shift
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/$name -o run --output-format csv -- \
+      python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 10 --warmup 2 $EXTRA > $OUT/$name.log 2>&1
+  echo "pmc $name rc=$?"
+}
+run fetch FETCH_SIZE || exit 1
+run write WRITE_SIZE || exit 1
+run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS GRBM_GUI_ACTIVE || exit 1
+run busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY || exit 1
+run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum || exit 1
