@@ -40,14 +40,13 @@ hipError_t ensure_aes_tables(hipStream_t stream)
     return g_tab_err[dev];
 }
 
-/* Lanes per record for ChaChaPoly: enough lanes in flight to give every
-   SIMD several waves (256 CUs x 16 waves x 64 lanes), never more than 8. */
+/* Lanes per record for ChaChaPoly: 4 (the fastest split at 64 Ki and 1 Mi
+   records, profiles/r01_sweep_*), 8 when the batch is too small to give every
+   SIMD four waves that way. */
 int auto_lanes(uint32_t n_records)
 {
     const uint64_t target = 256ull * 16 * 64;
-    int k = 1;
-    while (k < 8 && (uint64_t)n_records * k < target) k <<= 1;
-    return k;
+    return (uint64_t)n_records * 4 < target ? 8 : 4;
 }
 
 template <typename Args>
@@ -63,21 +62,33 @@ int launch(KernelFn<Args> fn, uint32_t n_records, int lanes, const Args &a, hipS
     return hip_rc(hipGetLastError());
 }
 
+template <int K>
+KernelFn<UniformArgs> chacha_staged_fn(bool open, bool ukey)
+{
+    if (ukey) return open ? chachapoly_open_staged<K, true> : chachapoly_seal_staged<K, true>;
+    return open ? chachapoly_open_staged<K, false> : chachapoly_seal_staged<K, false>;
+}
+
 template <bool FAST>
-KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open)
+KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey)
 {
     switch (k) {
     case 1: return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
     case 2: return open ? chachapoly_open_uniform<2, FAST> : chachapoly_seal_uniform<2, FAST>;
-    case 4: return open ? chachapoly_open_uniform<4, FAST> : chachapoly_seal_uniform<4, FAST>;
-    case 8: return open ? chachapoly_open_uniform<8, FAST> : chachapoly_seal_uniform<8, FAST>;
+    case 4:
+        if (FAST) return chacha_staged_fn<4>(open, ukey);
+        return open ? chachapoly_open_uniform<4, FAST> : chachapoly_seal_uniform<4, FAST>;
+    case 8:
+        if (FAST) return chacha_staged_fn<8>(open, ukey);
+        return open ? chachapoly_open_uniform<8, FAST> : chachapoly_seal_uniform<8, FAST>;
     }
     return nullptr;
 }
 
-KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast)
+/* ukey: every wave's 64/k records share one state (see u_key_nonce) */
+KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast, bool ukey)
 {
-    return fast ? chacha_uniform_fn_t<true>(k, open) : chacha_uniform_fn_t<false>(k, open);
+    return fast ? chacha_uniform_fn_t<true>(k, open, ukey) : chacha_uniform_fn_t<false>(k, open, ukey);
 }
 
 template <bool FAST>
@@ -147,7 +158,8 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     const UniformArgs a = to_args(job);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records);
-        KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open));
+        const bool ukey = k >= 4 && job->recs_per_state % (64u / (uint32_t)k) == 0;
+        KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open), ukey);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
         return launch(fn, job->n_records, k, a, s);
     }
@@ -156,8 +168,11 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
             return NOISE_ERROR_INVALID_PARAM;
         rc = hip_rc(ensure_aes_tables(s));
         if (rc) return rc;
-        return launch(open ? gcm_uniform<true> : gcm_uniform<false>, job->n_records,
-                      GCM_LANES, a, s);
+        /* one state per 64-record workgroup + FAST layout -> LDS-staged kernel */
+        const bool staged = uniform_fast(job, open) && job->recs_per_state % 64 == 0;
+        KernelFn<UniformArgs> fn = staged ? (open ? gcm_staged<true> : gcm_staged<false>)
+                                          : (open ? gcm_uniform<true> : gcm_uniform<false>);
+        return launch(fn, job->n_records, GCM_LANES, a, s);
     }
     return NOISE_ERROR_UNKNOWN_ID;
 }

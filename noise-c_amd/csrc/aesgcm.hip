@@ -346,4 +346,160 @@ __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
     if (OPEN && l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
+/* ------------------------------------- staged (uniform FAST, one state per WG)
+ *
+ * For uniform batches whose 64 records per workgroup share one CipherState
+ * (recs_per_state a multiple of 64) and FAST layouts.  The workgroup copies
+ * into LDS once: the four T-tables Te0..Te3 (no rotates in the rounds), the
+ * state's round keys, and its multiply-by-H^4 GHASH table (the Horner step),
+ * so the per-block work touches no global memory but the record bytes.  The
+ * record's data blocks are 16-B aligned dwordx4 loads/stores; the input is
+ * loaded at the top of each step and consumed after the AES block.
+ */
+struct GcmLds {
+    uint32_t te[4][256]; /* te[k][x] = rotr(Te0[x], 8k) */
+    uint4 h4[GHASH_TAB_ENTRIES];
+    uint32_t rk[60];
+};
+
+NA_DEV void gcm_lds_fill(GcmLds &L, const AesCtx *ctx)
+{
+    const int t = threadIdx.x;
+    const uint32_t e = g_te0[t];
+    L.te[0][t] = e; L.te[1][t] = rotr(e, 8); L.te[2][t] = rotr(e, 16); L.te[3][t] = rotr(e, 24);
+    const uint4 *src = (const uint4 *)ctx->tab[GCM_LANES - 1];
+    for (int i = t; i < GHASH_TAB_ENTRIES; i += 256) L.h4[i] = src[i];
+    if (t < 60) L.rk[t] = ctx->rk[t];
+    __syncthreads();
+}
+
+NA_DEV void aes256_lds(const GcmLds &L, uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3)
+{
+    const uint32_t *rk = L.rk;
+    s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+#pragma unroll
+    for (int r = 1; r < 14; ++r) {
+        const uint32_t t0 = L.te[0][s0 >> 24] ^ L.te[1][(s1 >> 16) & 255] ^
+                            L.te[2][(s2 >> 8) & 255] ^ L.te[3][s3 & 255] ^ rk[4 * r];
+        const uint32_t t1 = L.te[0][s1 >> 24] ^ L.te[1][(s2 >> 16) & 255] ^
+                            L.te[2][(s3 >> 8) & 255] ^ L.te[3][s0 & 255] ^ rk[4 * r + 1];
+        const uint32_t t2 = L.te[0][s2 >> 24] ^ L.te[1][(s3 >> 16) & 255] ^
+                            L.te[2][(s0 >> 8) & 255] ^ L.te[3][s1 & 255] ^ rk[4 * r + 2];
+        const uint32_t t3 = L.te[0][s3 >> 24] ^ L.te[1][(s0 >> 16) & 255] ^
+                            L.te[2][(s1 >> 8) & 255] ^ L.te[3][s2 & 255] ^ rk[4 * r + 3];
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    /* last round: S-box bytes picked out of the T-tables (Te0 = [2s,s,s,3s]) */
+#define NA_SB4(a, b, c, d)                                                        \
+    ((L.te[2][(a) >> 24] & 0xff000000u) | (L.te[3][((b) >> 16) & 255] & 0x00ff0000u) | \
+     (L.te[0][((c) >> 8) & 255] & 0x0000ff00u) | (L.te[1][(d) & 255] & 0x000000ffu))
+    const uint32_t o0 = NA_SB4(s0, s1, s2, s3), o1 = NA_SB4(s1, s2, s3, s0);
+    const uint32_t o2 = NA_SB4(s2, s3, s0, s1), o3 = NA_SB4(s3, s0, s1, s2);
+#undef NA_SB4
+    s0 = o0 ^ rk[56]; s1 = o1 ^ rk[57]; s2 = o2 ^ rk[58]; s3 = o3 ^ rk[59];
+}
+
+NA_DEV void aes_ctr_lds(const GcmLds &L, uint32_t n_hi, uint32_t n_lo, uint32_t ctr, uint32_t ks[4])
+{
+    uint32_t s0 = 0, s1 = n_hi, s2 = n_lo, s3 = ctr;
+    aes256_lds(L, s0, s1, s2, s3);
+    ks[0] = __builtin_bswap32(s0); ks[1] = __builtin_bswap32(s1);
+    ks[2] = __builtin_bswap32(s2); ks[3] = __builtin_bswap32(s3);
+}
+
+/* byte mask of the first nb (0..16) bytes of a 16-B block, word w */
+NA_DEV uint32_t blk_mask(uint32_t nb, int w)
+{
+    const int rb = (int)nb - 4 * w;
+    return rb >= 4 ? 0xffffffffu : (rb <= 0 ? 0u : ((1u << (8 * rb)) - 1u));
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(256) void gcm_staged(UniformArgs a)
+{
+    constexpr int K = GCM_LANES;
+    __shared__ GcmLds L;
+    const uint32_t rec0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (256u / K));
+    const uint32_t st = rec0 / a.rps; /* one state per workgroup (host-checked) */
+    const AesCtx *ctx = (const AesCtx *)a.keys + st;
+    gcm_lds_fill(L, ctx);
+
+    const uint32_t rec = rec0 + threadIdx.x / K;
+    if (rec >= a.n_records) return;
+    const int l = (int)(threadIdx.x % K);
+    const uint64_t nonce = a.nonce_base[st] + (uint64_t)(rec - st * a.rps);
+    const uint32_t n_hi = (uint32_t)(nonce >> 32), n_lo = (uint32_t)nonce;
+    const uint8_t *src = a.in + (size_t)rec * a.in_stride;
+    uint8_t *dst = a.out + (size_t)rec * a.out_stride;
+    const uint32_t len = a.len, ad_len = a.ad_len;
+    const uint32_t A = (ad_len + 15) / 16, M = (len + 15) / 16;
+    const uint32_t n = A + M + 1;
+    const uint32_t c0 = ((uint32_t)l + n) % K;
+
+    /* GHASH (and, sealing, CTR) over this lane's blocks i = c0, c0+K, ... */
+    uint32_t acc[4] = {0, 0, 0, 0};
+    for (uint32_t i = c0; i < n; i += K) {
+        if (i != c0) gh_mul(acc, L.h4);
+        uint32_t x[4];
+        if (i >= A && i < A + M) {
+            const uint32_t d = i - A;
+            const uint4 v = *(const uint4 *)(src + 16 * d); /* FAST: readable */
+            x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+            const uint32_t nb = min(len - 16 * d, 16u);
+            if (!OPEN) {
+                uint32_t ks[4];
+                aes_ctr_lds(L, n_hi, n_lo, 2 + d, ks);
+#pragma unroll
+                for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+                if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
+                else store16(dst + 16 * d, nb, x);
+            }
+#pragma unroll
+            for (int w = 0; w < 4; ++w) x[w] &= blk_mask(nb, w);
+        } else if (i < A) {
+            const uint32_t rem = ad_len - 16 * i;
+            load16(a.ad + (size_t)rec * a.ad_stride + 16 * i, rem >= 16 ? 16u : rem, x);
+        } else {
+            const uint64_t ab = (uint64_t)ad_len * 8, cb = (uint64_t)len * 8;
+            x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
+            x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
+        }
+        acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
+    }
+    /* scale by H^(K-l): lane K-1 by H, from the context's tables (once) */
+    gh_mul(acc, (const uint4 *)ctx->tab[K - 1 - l]);
+#pragma unroll
+    for (int off = 1; off < K; off <<= 1)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+    uint32_t ej[4];
+    aes_ctr_lds(L, n_hi, n_lo, 1u, ej);
+    const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
+    if (!OPEN) {
+        if (l == K - 1) {
+            if ((len & 15) == 0) *(uint4 *)(dst + len) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+            else if ((len & 7) == 0) {
+                *(uint2 *)(dst + len) = make_uint2(tag[0], tag[1]);
+                *(uint2 *)(dst + len + 8) = make_uint2(tag[2], tag[3]);
+            } else store16(dst + len, 16, tag);
+        }
+        return;
+    }
+    uint32_t got[4];
+    load16(src + len, 16, got);
+    const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) == 0;
+    if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (!ok) return; /* cipher-aesgcm.c:184-186: nothing decrypted */
+    for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
+        const uint4 v = *(const uint4 *)(src + 16 * d);
+        uint32_t x[4] = {v.x, v.y, v.z, v.w}, ks[4];
+        aes_ctr_lds(L, n_hi, n_lo, 2 + d, ks);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+        const uint32_t nb = min(len - 16 * d, 16u);
+        if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
+        else store16(dst + 16 * d, nb, x);
+    }
+}
+
 } // namespace na

@@ -476,174 +476,276 @@ NA_DEV void tile_put_unit(uint4 *t, uint32_t L, const uint32_t w[16])
 }
 
 /* The wave's coalesced view: for instruction i, this lane serves owner
-   L = 16i + lane/4 — record rec0 + L/K, unit offset L%K, chunk lane%4. */
+   L = 16i + lane/4 — record rq + i*16/K, unit offset kk = L%K (the same for
+   all four i since K | 16), chunk lane%4.  Addresses are rebuilt from the
+   kernel arguments at each use instead of being held in 16 VGPRs. */
 template <int K>
 struct WaveIO {
-    const uint8_t *in[4];
-    uint8_t *out[4];
-    uint32_t kk[4];
-    bool live[4];
+    uint32_t rq;   /* record of instruction 0 (unclamped) */
+    uint32_t c16;  /* byte offset of this lane's chunk (register-staged) */
+    uint32_t d16;  /* byte offset of the chunk this lane DMAs (see wave_dma) */
+    int kk;
 };
 
 template <int K>
-NA_DEV WaveIO<K> wave_io(const UniformArgs &a, uint32_t rec0, uint32_t lane)
+NA_DEV WaveIO<K> wave_io(uint32_t rec0, uint32_t lane)
 {
     WaveIO<K> io;
-    const uint32_t c = lane & 3;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t L = 16u * i + (lane >> 2);
-        const uint32_t r = rec0 + L / K;
-        io.live[i] = r < a.n_records;
-        const uint32_t rc = io.live[i] ? r : a.n_records - 1;
-        io.in[i] = a.in + (size_t)rc * a.in_stride + 16 * c;
-        io.out[i] = a.out + (size_t)rc * a.out_stride + 16 * c;
-        io.kk[i] = L % K;
-    }
+    io.rq = rec0 + (lane >> 2) / K;
+    io.c16 = 16u * (lane & 3);
+    io.d16 = 16u * ((lane ^ (lane >> 4)) & 3);
+    io.kk = (int)((lane >> 2) % K);
     return io;
 }
 
-/* Coalesced loads of step unit base j0 (unit of owner offset kk = j0 + kk,
-   clamped to unit 0 where it does not exist). */
 template <int K>
-NA_DEV Quad wave_load(const WaveIO<K> &io, int j0)
+NA_DEV uint32_t wave_rec(const WaveIO<K> &io, int i) { return io.rq + (uint32_t)i * (16 / K); }
+
+/* Coalesced loads of the step with unit base j0 (owner unit j0 + kk, clamped
+   to unit 0 below the record start, records clamped to the batch end). */
+template <int K>
+NA_DEV Quad wave_load(const UniformArgs &a, const WaveIO<K> &io, int j0)
 {
-    int u0 = j0 + (int)io.kk[0], u1 = j0 + (int)io.kk[1];
-    int u2 = j0 + (int)io.kk[2], u3 = j0 + (int)io.kk[3];
+    const int u = j0 + io.kk;
+    const uint32_t off = io.c16 + 64u * (uint32_t)(u > 0 ? u : 0);
+    const uint32_t last = a.n_records - 1;
     Quad P;
-    P.a = *(const uint4 *)(io.in[0] + 64 * (u0 > 0 ? u0 : 0));
-    P.b = *(const uint4 *)(io.in[1] + 64 * (u1 > 0 ? u1 : 0));
-    P.c = *(const uint4 *)(io.in[2] + 64 * (u2 > 0 ? u2 : 0));
-    P.d = *(const uint4 *)(io.in[3] + 64 * (u3 > 0 ? u3 : 0));
+    P.a = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 0), last) * a.in_stride + off);
+    P.b = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 1), last) * a.in_stride + off);
+    P.c = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 2), last) * a.in_stride + off);
+    P.d = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 3), last) * a.in_stride + off);
     return P;
 }
 
+typedef __attribute__((address_space(3))) void lds_void;
+
+/* The same step as wave_load, but straight into the tile by LDS-DMA
+   (global_load_lds_dwordx4: no VGPRs, no ds_write).  The DMA fills the tile
+   lane-linearly (slot 64i + lane), so the tile_slot swizzle moves to the
+   source: slot 64i + l holds owner L = 16i + l/4, chunk (l ^ l>>4) & 3. */
 template <int K>
-NA_DEV void wave_store(const WaveIO<K> &io, int j0, int last_full, const uint4 *t, uint32_t lane,
-                       const bool okL[4])
+NA_DEV void wave_dma(const UniformArgs &a, const WaveIO<K> &io, int j0, uint4 *t)
 {
+    const int u = j0 + io.kk;
+    const uint32_t off = io.d16 + 64u * (uint32_t)(u > 0 ? u : 0);
+    const uint32_t last = a.n_records - 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(a.in + (size_t)min(wave_rec(io, i), last) * a.in_stride + off),
+            (lds_void *)(t + 64 * i), 16, 0, 0);
+}
+
+/* Coalesced stores of the step's full units (unit <= last_full) from the
+   tile; okm bit i gates instruction i (open: the owner's verdict). */
+template <int K>
+NA_DEV void wave_store(const UniformArgs &a, const WaveIO<K> &io, int j0, int last_full,
+                       const uint4 *t, uint32_t lane, uint32_t okm)
+{
+    const int u = j0 + io.kk;
+    if (u < 0 || u > last_full) return;
+    const uint32_t off = io.c16 + 64u * (uint32_t)u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint4 q = t[tile_slot(16u * i + (lane >> 2), lane & 3)];
-        const int u = j0 + (int)io.kk[i];
-        if (io.live[i] && okL[i] && u >= 0 && u <= last_full) *(uint4 *)(io.out[i] + 64 * u) = q;
+        const uint32_t r = wave_rec(io, i);
+        if (r < a.n_records && ((okm >> i) & 1))
+            *(uint4 *)(a.out + (size_t)r * a.out_stride + off) = q;
     }
 }
 
-template <int K>
-NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tile)
+/* FAST exact-size store of a record's last unit: nb (1..64) bytes at p
+   (16-B aligned). */
+NA_DEV void last_unit_out(uint8_t *p, uint32_t nb, const uint32_t w[16])
+{
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c)
+        if (16 * c + 16 <= nb)
+            *(uint4 *)(p + 16 * c) = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+    const uint32_t rem = nb & 15;
+    if (rem) {
+        uint32_t part[4];
+        pick_chunk(w, nb >> 4, part);
+        uint8_t *q = p + (nb & ~15u);
+        if (rem == 8) *(uint2 *)q = make_uint2(part[0], part[1]);
+        else store16(q, rem, part);
+    }
+}
+
+/* FAST tag store at p = record + len (p is 16-B aligned iff len % 16 == 0). */
+NA_DEV void tag_out(uint8_t *p, uint32_t len, const uint32_t t[4])
+{
+    if ((len & 15) == 0) {
+        *(uint4 *)p = make_uint4(t[0], t[1], t[2], t[3]);
+    } else if ((len & 7) == 0) {
+        *(uint2 *)p = make_uint2(t[0], t[1]);
+        *(uint2 *)(p + 8) = make_uint2(t[2], t[3]);
+    } else {
+        store16(p, 16, t);
+    }
+}
+
+/* Per-lane scratch the staged seal kernel parks outside its loop: lane k's
+   final Poly1305 scale (an Fe), written at step 0 and read after the loop so
+   it is not held in 5 VGPRs across the ChaCha blocks. */
+struct FinSlot { uint32_t l[5][64]; };
+
+NA_DEV void fin_put(FinSlot *f, uint32_t lane, const Mul &m)
+{
+    f->l[0][lane] = m.r0; f->l[1][lane] = m.r1; f->l[2][lane] = m.r2;
+    f->l[3][lane] = m.r3; f->l[4][lane] = m.r4;
+}
+
+NA_DEV Mul fin_get(const FinSlot *f, uint32_t lane)
+{
+    return mk_mul(Fe{f->l[0][lane], f->l[1][lane], f->l[2][lane], f->l[3][lane], f->l[4][lane]});
+}
+
+/* Record pointers of the uniform batch, rebuilt at each use (a handful of
+   VALU) instead of being held in 64-bit VGPR pairs across the loop. */
+NA_DEV const uint8_t *u_src(const UniformArgs &a, uint32_t rc) { return a.in + (size_t)rc * a.in_stride; }
+NA_DEV uint8_t *u_dst(const UniformArgs &a, uint32_t rc) { return a.out + (size_t)rc * a.out_stride; }
+NA_DEV const uint8_t *u_ad(const UniformArgs &a, uint32_t rc) { return a.ad + (size_t)rc * a.ad_stride; }
+
+/* Key and nonce of record rc.  UKEY: the host guarantees that all records of
+   a wave share one CipherState (recs_per_state a multiple of 64/K), so the
+   key is wave-uniform and lives in SGPRs — 8 VGPRs the loop keeps free. */
+template <bool UKEY>
+NA_DEV void u_key_nonce(const UniformArgs &a, uint32_t rec0, uint32_t rc, uint32_t key[8],
+                        uint32_t &n_lo, uint32_t &n_hi)
+{
+    uint64_t n;
+    if constexpr (UKEY) {
+        const uint32_t st = __builtin_amdgcn_readfirstlane(rec0) / a.rps;
+        load_key(a.keys + (size_t)st * 32, key);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) key[i] = __builtin_amdgcn_readfirstlane(key[i]);
+        n = a.nonce_base[st] + (uint64_t)(rc - st * a.rps);
+    } else {
+        const uint32_t st = rc / a.rps;
+        load_key(a.keys + (size_t)st * 32, key);
+        n = a.nonce_base[st] + (uint64_t)(rc - st * a.rps);
+    }
+    n_lo = (uint32_t)n;
+    n_hi = (uint32_t)(n >> 32);
+}
+
+template <int K, bool UKEY>
+NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin)
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t rec0 = ((blockIdx.x * 256u + threadIdx.x) >> 6) * (64 / K);
     const uint32_t rec_raw = rec0 + lane / K;
     const bool live = rec_raw < a.n_records;
-    const RecView rv = uniform_view(a, live ? rec_raw : a.n_records - 1);
+    const uint32_t rc = live ? rec_raw : a.n_records - 1;
     const int k = (int)(lane % K);
-    uint32_t key[8];
-    load_key(rv.key, key);
-    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
-    const uint32_t len = rv.len;
-    const GroupCtx<K> g = group_ctx<K>(len);
+    uint32_t key[8], n_lo, n_hi;
+    u_key_nonce<UKEY>(a, rec0, rc, key, n_lo, n_hi);
+    const uint32_t len = a.len;
+    const GroupCtx<K> g = group_ctx<K>(len); /* wave-uniform (uniform batch) */
     const int gbase = (int)lane & ~(K - 1);
-    const WaveIO<K> io = wave_io<K>(a, rec0, lane);
-    const bool all_ok[4] = {true, true, true, true};
-    const int last_full = (int)g.J - 2; /* unit J-1 is the tail, stored after */
+    const WaveIO<K> io = wave_io<K>(rec0, lane);
+    const int last_full = (int)g.J - 2; /* unit J-1 is stored by its owner */
 
-    Fe acc = fe_zero(), r;
-    Mul mr, mjump, mfinal;
-    uint32_t s[4], x[16], wt[16];
+    Fe acc = fe_zero();
+    Mul mr, mjump;
+    uint32_t s[4];
     bool seen = false;
-    Quad P = wave_load<K>(io, -(int)g.o - 1);
-    tile_put_coalesced(tile, lane, P);
+    wave_dma<K>(a, io, -(int)g.o - 1, tiles);
     for (uint32_t m = 0; m < g.steps; ++m) {
         const int j0 = (int)(m * K) - (int)g.o - 1;
         const int v = j0 + 1 + k;
+        uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
         __builtin_amdgcn_wave_barrier();
-        uint32_t w[16];
-        tile_get_unit(tile, lane, w);
-        __builtin_amdgcn_wave_barrier();
-        /* next step's bytes: issued now, parked in the tile at the end of
-           this iteration — no loop-carried load registers, so hipcc's wait
-           lands after the ChaCha block instead of right after the loads */
-        const bool more = m + 1 < g.steps;
-        P = wave_load<K>(io, more ? j0 + K : j0);
+        /* next step's bytes go into the other tile while this one computes */
+        if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
+        uint32_t x[16];
         chacha20_block(key, (uint32_t)v, 0u, n_lo, n_hi, x);
         if (m == 0) {
+            Fe r;
             poly_key_bcast(x, gbase + (int)g.o, r, s);
             mr = mk_mul(r);
+            Mul mfinal;
             poly_powers<K>(r, k, g.q, mjump, mfinal);
+            fin_put(fin, lane, mfinal);
             const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
-            if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
+            if (k == k0 && a.ad_len) poly_ad(acc, mr, u_ad(a, rc), a.ad_len);
         }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t w[16];
+        tile_get_unit(cur, lane, w);
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-        if (v >= 1 && (uint32_t)v < g.J) {
-            poly_unit(acc, seen ? mjump : mr, mr, w, 4);
+        if (v >= 1 && (uint32_t)v <= g.J) {
+            /* one Poly path for full units and the last (lane K-1's last
+               step), so a wave never runs both */
+            uint32_t nb = 4;
+            if ((uint32_t)v == g.J) {
+                const uint32_t bytes = len - 64 * (g.J - 1);
+                if (live) last_unit_out(u_dst(a, rc) + 64 * (g.J - 1), bytes, w);
+                mask_unit(w, bytes);
+                nb = (bytes + 15) / 16;
+            }
+            poly_unit(acc, seen ? mjump : mr, mr, w, nb);
             seen = true;
         }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) wt[i] = w[i];
-        tile_put_unit(tile, lane, w);
+        tile_put_unit(cur, lane, w);
         __builtin_amdgcn_wave_barrier();
-        wave_store<K>(io, j0, last_full, tile, lane, all_ok);
-        __builtin_amdgcn_wave_barrier();
-        tile_put_coalesced(tile, lane, P); /* harmless after the last step */
-    }
-    /* the last unit (block J) is lane K-1's last step */
-    if (k == K - 1 && g.J >= 1) {
-        const uint32_t nb = len - 64 * (g.J - 1);
-        mask_unit(wt, nb);
-        poly_unit(acc, seen ? mjump : mr, mr, wt, (nb + 15) / 16);
+        wave_store<K>(a, io, j0, last_full, cur, lane, 0xfu);
     }
     uint32_t tag[4];
-    poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
-    if (k == K - 1 && live) tail_out<true, true>(rv.dst, g.J, len, wt, tag);
+    poly_close<K>(acc, k, mr, fin_get(fin, lane), a.ad_len, len, s, tag);
+    if (k == K - 1 && live) tag_out(u_dst(a, rc) + len, len, tag);
 }
 
-template <int K>
-NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tile)
+template <int K, bool UKEY>
+NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles)
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t rec0 = ((blockIdx.x * 256u + threadIdx.x) >> 6) * (64 / K);
     const uint32_t rec_raw = rec0 + lane / K;
     const bool live = rec_raw < a.n_records;
-    const RecView rv = uniform_view(a, live ? rec_raw : a.n_records - 1);
+    const uint32_t rc = live ? rec_raw : a.n_records - 1;
     const int k = (int)(lane % K);
-    uint32_t key[8];
-    load_key(rv.key, key);
-    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
-    const uint32_t len = rv.len;
+    uint32_t key[8], n_lo, n_hi;
+    u_key_nonce<UKEY>(a, rec0, rc, key, n_lo, n_hi);
+    const uint32_t len = a.len;
     const GroupCtx<K> g = group_ctx<K>(len);
     const int gbase = (int)lane & ~(K - 1);
-    const WaveIO<K> io = wave_io<K>(a, rec0, lane);
+    const WaveIO<K> io = wave_io<K>(rec0, lane);
     const int last_full = (int)g.J - 2;
+    uint4 *const t0 = tiles, *const t1 = tiles + 256;
 
+    /* step-0 key stream: block 0 (Poly key) on lane o, data on the others;
+       parked in tile 1 until phase 2 */
     const int v0 = k - (int)g.o;
-    uint32_t x0[16];
-    chacha20_block(key, (uint32_t)v0, 0u, n_lo, n_hi, x0);
-    Fe r;
-    uint32_t s[4];
-    poly_key_bcast(x0, gbase + (int)g.o, r, s);
-    const Mul mr = mk_mul(r);
-    Mul mjump, mfinal;
-    poly_powers<K>(r, k, g.q, mjump, mfinal);
     Fe acc = fe_zero();
+    Mul mr, mjump, mfinal;
+    uint32_t s[4];
+    {
+        uint32_t x0[16];
+        chacha20_block(key, (uint32_t)v0, 0u, n_lo, n_hi, x0);
+        tile_put_unit(t1, lane, x0);
+        Fe r;
+        poly_key_bcast(x0, gbase + (int)g.o, r, s);
+        mr = mk_mul(r);
+        poly_powers<K>(r, k, g.q, mjump, mfinal);
+    }
     const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
-    if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
+    if (k == k0 && a.ad_len) poly_ad(acc, mr, u_ad(a, rc), a.ad_len);
 
-    /* phase 1: authenticate */
+    /* phase 1: authenticate.  No ChaCha to hide behind here, so the next
+       step is register-prefetched and tile 0 alone is used. */
     bool seen = false;
-    Quad P = wave_load<K>(io, -(int)g.o - 1);
-    tile_put_coalesced(tile, lane, P);
+    Quad P = wave_load<K>(a, io, -(int)g.o - 1);
+    tile_put_coalesced(t0, lane, P);
     for (uint32_t m = 0; m < g.steps; ++m) {
         const int j0 = (int)(m * K) - (int)g.o - 1;
         const int v = j0 + 1 + k;
+        P = wave_load<K>(a, io, m + 1 < g.steps ? j0 + K : j0);
         __builtin_amdgcn_wave_barrier();
         uint32_t w[16];
-        tile_get_unit(tile, lane, w);
-        __builtin_amdgcn_wave_barrier();
-        const bool more = m + 1 < g.steps;
-        P = wave_load<K>(io, more ? j0 + K : j0);
+        tile_get_unit(t0, lane, w);
         if (v >= 1) {
             uint32_t nb = 4;
             if ((uint32_t)v == g.J) {
@@ -655,46 +757,46 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tile)
             seen = true;
         }
         __builtin_amdgcn_wave_barrier();
-        tile_put_coalesced(tile, lane, P); /* harmless after the last step */
+        tile_put_coalesced(t0, lane, P);
     }
     uint32_t tag[4], got[4];
-    poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
-    tag_in<true>(rv.src, len, got);
+    poly_close<K>(acc, k, mr, mfinal, a.ad_len, len, s, tag);
+    tag_in<true>(u_src(a, rc), len, got);
     const bool ok = tag_equal(tag, got);
     if (k == K - 1 && live && a.status) a.status[rec_raw] = ok ? 0 : 1;
-    /* verdict of the owner each coalesced slot serves */
-    bool okL[4];
+    /* verdict of the owner each coalesced instruction serves */
+    uint32_t okm = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) okL[i] = __shfl((int)ok, (int)(16u * i + (lane >> 2)), 64) != 0;
+    for (int i = 0; i < 4; ++i)
+        okm |= (__shfl((int)ok, (int)(16u * i + (lane >> 2)), 64) != 0 ? 1u : 0u) << i;
 
-    /* phase 2: decrypt (wave-uniform: every lane joins the exchanges) */
-    uint32_t x[16], wt[16];
-    P = wave_load<K>(io, -(int)g.o - 1);
-    tile_put_coalesced(tile, lane, P);
+    /* phase 2: decrypt, double-buffered by LDS-DMA (the step-0 key stream
+       leaves tile 1 before the first DMA into it) */
+    __builtin_amdgcn_wave_barrier();
+    wave_dma<K>(a, io, -(int)g.o - 1, t0);
     for (uint32_t m = 0; m < g.steps; ++m) {
         const int j0 = (int)(m * K) - (int)g.o - 1;
         const int v = j0 + 1 + k;
+        uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
+        uint32_t x[16];
+        if (m == 0) {
+            tile_get_unit(t1, lane, x);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
+        if (m != 0) chacha20_block(key, (uint32_t)v, 0u, n_lo, n_hi, x);
         __builtin_amdgcn_wave_barrier();
         uint32_t w[16];
-        tile_get_unit(tile, lane, w);
-        __builtin_amdgcn_wave_barrier();
-        const bool more = m + 1 < g.steps;
-        P = wave_load<K>(io, more ? j0 + K : j0);
-        if (m == 0) {
+        tile_get_unit(cur, lane, w);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) x[i] = x0[i];
-        } else {
-            chacha20_block(key, (uint32_t)v, 0u, n_lo, n_hi, x);
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) wt[i] = w[i] ^ x[i];
-        tile_put_unit(tile, lane, wt);
+        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+        if (v >= 1 && (uint32_t)v == g.J && live && ok)
+            last_unit_out(u_dst(a, rc) + 64 * (g.J - 1), len - 64 * (g.J - 1), w);
+        tile_put_unit(cur, lane, w);
         __builtin_amdgcn_wave_barrier();
-        wave_store<K>(io, j0, last_full, tile, lane, okL);
-        __builtin_amdgcn_wave_barrier();
-        tile_put_coalesced(tile, lane, P); /* harmless after the last step */
+        wave_store<K>(a, io, j0, last_full, cur, lane, okm);
     }
-    if (k == K - 1 && live && ok && g.J >= 1) tail_out<true, false>(rv.dst, g.J, len, wt, nullptr);
 }
 
 /* ------------------------------------------------- contiguous (K = 1, 2) */
@@ -881,6 +983,12 @@ NA_DEV bool open_ct(const RecView &rv, int k)
 
 /* ------------------------------------------------------------- kernels */
 
+/* 4 waves per SIMD: one C2-sized batch (64 Ki records, 4 lanes each) is then
+   exactly one resident round of the 1024 SIMDs */
+#ifndef NA_UNIFORM_OCC
+#define NA_UNIFORM_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+
 /* lanes per record: 1 or 2 -> contiguous runs, 4 or 8 -> interleaved units */
 template <int K, bool FAST>
 NA_DEV void seal_any(const RecView &rv, int k)
@@ -924,14 +1032,25 @@ NA_DEV RecView ragged_view(const RaggedArgs &a, uint32_t rec)
     return rv;
 }
 
+/* LDS-staged uniform FAST batches, K = 4 or 8 lanes per record */
+template <int K, bool UKEY>
+__global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_seal_staged(UniformArgs a)
+{
+    __shared__ uint4 tiles[4][512]; /* two 4 KB tiles per wave */
+    __shared__ FinSlot fin[4];
+    seal_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6]);
+}
+
+template <int K, bool UKEY>
+__global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_open_staged(UniformArgs a)
+{
+    __shared__ uint4 tiles[4][512];
+    open_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6]);
+}
+
 template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_seal_uniform(UniformArgs a)
 {
-    if constexpr (K >= 4 && FAST) {
-        __shared__ uint4 tiles[4][256]; /* 4 KB per wave */
-        seal_il_staged<K>(a, tiles[threadIdx.x >> 6]);
-        return;
-    }
     const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t rec = gtid / K;
     if (rec >= a.n_records) return; /* whole groups leave together (K | 64) */
@@ -941,11 +1060,6 @@ __global__ __launch_bounds__(256) void chachapoly_seal_uniform(UniformArgs a)
 template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_open_uniform(UniformArgs a)
 {
-    if constexpr (K >= 4 && FAST) {
-        __shared__ uint4 tiles[4][256];
-        open_il_staged<K>(a, tiles[threadIdx.x >> 6]);
-        return;
-    }
     const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
     const uint32_t rec = gtid / K;
     if (rec >= a.n_records) return;

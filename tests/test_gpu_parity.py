@@ -107,10 +107,13 @@ LENS = [0, 1, 15, 16, 17, 48, 56, 63, 64, 65, 127, 128, 129, 191, 192, 255, 256,
 @pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 2), (CHACHA, 4), (CHACHA, 8),
                                           (AES, 0)])
 @pytest.mark.parametrize("packed", [False, True])
-def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed):
-    rng = np.random.default_rng(1000 + lanes + 7 * packed + (cipher & 3))
+@pytest.mark.parametrize("rps", [13, 16])
+def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed, rps):
+    """rps=13: states straddle waves; rps=16: every 4/8-lane wave holds one
+    state (the wave-uniform-key kernels), the last wave partial."""
+    rng = np.random.default_rng(1000 + lanes + 7 * packed + (cipher & 3) + rps)
     for L in LENS:
-        count, rps = 37, 13  # 3 states, the last one partial
+        count = 37 if rps == 13 else 70  # the last state partial
         S = (count + rps - 1) // rps
         keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
         nb = rng.integers(0, 2**63, S, dtype=np.uint64) * 2
@@ -140,11 +143,12 @@ def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed):
 
 
 @pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 4), (CHACHA, 8), (AES, 0)])
-def test_uniform_with_ad(aead, gpu, oracle, cipher, lanes):
-    rng = np.random.default_rng(77 + lanes)
+@pytest.mark.parametrize("rps", [4, 16])
+def test_uniform_with_ad(aead, gpu, oracle, cipher, lanes, rps):
+    rng = np.random.default_rng(77 + lanes + rps)
     for L in [0, 1, 64, 65, 1024, 1400]:
         for adl in [1, 12, 16, 32, 33, 100]:
-            count, rps = 9, 4
+            count = 2 * rps + 1
             S = 3
             keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
             nb = rng.integers(0, 2**40, S, dtype=np.uint64)
