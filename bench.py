@@ -43,7 +43,14 @@ CONFIGS = {
                workload="AES-256-GCM 64Ki x 1400B records, one CipherState key"),
     "c4": dict(cipher=CHACHA, records=1048576, len=1400, states=4096,
                workload="ChaCha20-Poly1305 1Mi x 1400B records, 4096 CipherStates x 256"),
+    # C5 per GPU = 1/8 of the 8-GPU job (1 Mi records, 4096 states in total):
+    # lengths 64 + splitmix64(seed_len + i) mod 16321, cipher by state parity.
+    "c5": dict(cipher=None, records=131072, len=None, states=512,
+               workload="Mixed ChaChaPoly (even states) + AESGCM (odd states), 64 B-16 KiB "
+                        "records (SURVEY.md 8d C5), 128 Ki records / 512 CipherStates per GPU, "
+                        "ragged descriptors"),
 }
+SEED_LEN, SEED_PT, SEED_KEY = 0x6C656E, 0x7074, 0x6B6579
 IN_ALIGN = 16  # device record strides are padded to 16 B (layout)
 
 
@@ -62,6 +69,36 @@ def shard(records_per_gpu: int, states: int, rank: int, world: int):
     key_ids = [rank * states + s for s in range(states)] if states > 1 else [0]
     return dict(first=first, count=records_per_gpu, rps=rps, nonce_base=nonce_base,
                 key_ids=key_ids)
+
+
+def splitmix64_np(x):
+    """SplitMix64 of uint64 array x (oracle_splitmix64)."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        z = x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def mixed_layout(records_per_gpu: int, states: int, rank: int):
+    """C5 shard of rank: global record i = rank*R + j, length
+    64 + splitmix64(SEED_LEN + i) % 16321, state rank*S + j // (R/S),
+    ChaChaPoly for even global states, AESGCM for odd; record slots are
+    roundup64(len + 16) bytes (FAST: 16-B aligned, readable past the tag)."""
+    import numpy as np
+    R, S = records_per_gpu, states
+    gi = np.arange(rank * R, (rank + 1) * R, dtype=np.uint64)
+    lens = (np.uint64(64) + splitmix64_np(np.uint64(SEED_LEN) + gi) % np.uint64(16321)).astype(np.int64)
+    slot = (lens + 16 + 63) // 64 * 64
+    off = np.zeros(R, dtype=np.int64)
+    off[1:] = np.cumsum(slot)[:-1]
+    rps = R // S
+    st_local = np.arange(R) // rps
+    st_global = rank * S + st_local
+    nonce = (np.arange(R) % rps).astype(np.uint64)
+    return dict(lens=lens, off=off, total=int(off[-1] + slot[-1]), st_local=st_local,
+                st_global=st_global, nonce=nonce, rps=rps)
 
 
 def stride(n: int) -> int:
@@ -142,6 +179,8 @@ def main():
     torch.cuda.set_device(dev)
 
     cfg = CONFIGS[args.config]
+    if args.config == "c5":
+        return run_mixed(args, cfg, A, torch, dev, rank, world, dist)
     cipher, N, L, S = cfg["cipher"], cfg["records"], cfg["len"], cfg["states"]
     sh = shard(N, S, rank, world)
     in_stride, out_stride = stride(L), stride(L + 16)
@@ -264,6 +303,120 @@ def main():
             result["cpu_baseline"] = cpu_baseline(cfg)
         except Exception as e:  # reported, never fatal to the GPU number
             result["cpu_baseline"] = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
+    """C5: mixed-cipher ragged batch, seal then open (tags verified)."""
+    import numpy as np
+    R, S = cfg["records"], cfg["states"]
+    lay = mixed_layout(R, S, rank)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    rec_dt = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "<u8"),
+                       ("ad_off", "<u8"), ("len", "<u4"), ("ad_len", "<u4")])
+    assert rec_dt.itemsize == 48
+    pt = torch.empty(lay["total"], dtype=torch.uint8, device=dev)
+    assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), SEED_PT, rank << 40, sp) == 0
+    ct = torch.empty_like(pt)
+    back = torch.empty_like(pt)
+    groups = []
+    for cipher, parity in ((CHACHA, 0), (AES, 1)):
+        states = [s for s in range(S) if (rank * S + s) % 2 == parity]
+        if not states:
+            continue
+        cb = A.dev_ctx_bytes(cipher)
+        raw = torch.empty(len(states) * 32, dtype=torch.uint8, device=dev)
+        for i, s in enumerate(states):
+            assert A.dev_fill_splitmix(raw[32 * i:].data_ptr(), 32, SEED_KEY, 4 * (rank * S + s), sp) == 0
+        ctx = torch.empty(len(states) * cb, dtype=torch.uint8, device=dev)
+        assert A.dev_prepare(cipher, raw.data_ptr(), len(states), ctx.data_ptr(), sp) == 0
+        slot_of = {s: i for i, s in enumerate(states)}
+        idx = np.nonzero((lay["st_global"] % 2) == parity)[0]
+        recs = np.zeros(len(idx), dtype=rec_dt)
+        recs["in_off"] = lay["off"][idx]
+        recs["out_off"] = lay["off"][idx]
+        recs["nonce"] = lay["nonce"][idx]
+        recs["ctx_off"] = np.array([slot_of[s] for s in lay["st_local"][idx]], dtype=np.uint64) * cb
+        recs["len"] = lay["lens"][idx]
+        d_recs = torch.from_numpy(recs.view(np.uint8)).to(dev)
+        st = torch.empty(len(idx), dtype=torch.uint8, device=dev)
+        groups.append(dict(cipher=cipher, ctx=ctx, recs=d_recs, n=len(idx), st=st,
+                           bytes=int(lay["lens"][idx].sum()), states=len(states)))
+    torch.cuda.synchronize(dev)
+
+    def launch(g, open_):
+        return A.dev_ragged(open_, g["cipher"], ctx_base=g["ctx"].data_ptr(),
+                            recs=g["recs"].data_ptr(), inp=(ct if open_ else pt).data_ptr(),
+                            out=(back if open_ else ct).data_ptr(), n_records=g["n"],
+                            status=g["st"].data_ptr() if open_ else 0, lanes=args.lanes,
+                            flags=A.FLAG_FAST, stream=sp)
+
+    def step():
+        for open_ in (False, True):
+            for g in groups:
+                rc = launch(g, open_)
+                if rc:
+                    raise RuntimeError(f"launch failed {rc:#x}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    # per-kernel times (separate, untimed pass) for the roofline line
+    per = []
+    for open_ in (False, True):
+        for g in groups:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                launch(g, open_)
+            e1.record()
+            torch.cuda.synchronize(dev)
+            per.append((e0.elapsed_time(e1) / 5, g, open_))
+    ok = all(bool((g["st"] == 0).all().item()) for g in groups)
+    if args.verify:  # round trip on a sample of records (statuses: all of them, above)
+        rng = np.random.default_rng(rank)
+        for j in rng.choice(R, size=min(512, R), replace=False):
+            o, n = int(lay["off"][j]), int(lay["lens"][j])
+            ok &= bool(torch.equal(back[o:o + n], pt[o:o + n]))
+    payload = sum(g["bytes"] for g in groups)
+    value = 2.0 * payload * world * args.steps / elapsed / GIB
+    ms, g, open_ = max(per, key=lambda x: x[0])
+    alg = 2 * g["bytes"] + 16 * g["n"] + 40 * g["states"]
+    achieved = alg / (ms * 1e-3) / 1e9
+    kname = ("chachapoly_" if g["cipher"] == CHACHA else "gcm_") + ("open" if open_ else "seal") + "_ragged"
+    result = {
+        "metric": "GiB/s device-resident AEAD encrypt+decrypt, mixed 64B-16KiB records per GPU",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (SplitMix64 lengths, plaintext and keys, SURVEY.md 8d C5), resident in HBM",
+        "config": {"workload": cfg["workload"], "config": "c5", "records_per_gpu": R,
+                   "states_per_gpu": S, "payload_bytes_per_step": int(2 * payload * world),
+                   "parallelism": f"states x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": kname, "algorithmic_bytes_per_launch": alg,
+                     "avg_launch_ms": round(ms, 5)},
+        "kernels_ms": {(("chacha" if gg["cipher"] == CHACHA else "aes") + ("_open" if o else "_seal")): round(m, 4)
+                       for m, gg, o in per},
+        "all_tags_verified": ok,
+    }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -118,6 +118,25 @@ NA_DEV void gh_mul(uint32_t y[4], const uint4 *__restrict__ tab)
     y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
 }
 
+NA_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+/* gh_mul with the table in LDS: lookups taken in pairs so every accumulate is
+   one 3-input XOR */
+NA_DEV void gh_mul_lds(uint32_t y[4], const uint4 *tab)
+{
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+#pragma unroll
+    for (int p = 0; p < 32; p += 2) {
+        const int b = p >> 1; /* byte b: high nibble is position p, low nibble p+1 */
+        const uint32_t byte = (y[b >> 2] >> (8 * (b & 3))) & 255u;
+        const uint4 e = tab[p * 16 + (byte >> 4)];
+        const uint4 f = tab[(p + 1) * 16 + (byte & 15)];
+        r0 = xor3(r0, e.x, f.x); r1 = xor3(r1, e.y, f.y);
+        r2 = xor3(r2, e.z, f.z); r3 = xor3(r3, e.w, f.w);
+    }
+    y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
+}
+
 /* ----------------------------------------------------------- key prepare */
 
 /* Byte-serial GF(2^128) helpers for the (once per key) table build. */
@@ -379,14 +398,15 @@ NA_DEV void aes256_lds(const GcmLds &L, uint32_t &s0, uint32_t &s1, uint32_t &s2
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
-        const uint32_t t0 = L.te[0][s0 >> 24] ^ L.te[1][(s1 >> 16) & 255] ^
-                            L.te[2][(s2 >> 8) & 255] ^ L.te[3][s3 & 255] ^ rk[4 * r];
-        const uint32_t t1 = L.te[0][s1 >> 24] ^ L.te[1][(s2 >> 16) & 255] ^
-                            L.te[2][(s3 >> 8) & 255] ^ L.te[3][s0 & 255] ^ rk[4 * r + 1];
-        const uint32_t t2 = L.te[0][s2 >> 24] ^ L.te[1][(s3 >> 16) & 255] ^
-                            L.te[2][(s0 >> 8) & 255] ^ L.te[3][s1 & 255] ^ rk[4 * r + 2];
-        const uint32_t t3 = L.te[0][s3 >> 24] ^ L.te[1][(s0 >> 16) & 255] ^
-                            L.te[2][(s1 >> 8) & 255] ^ L.te[3][s2 & 255] ^ rk[4 * r + 3];
+        /* 5-input XOR as two v_bitop3 (3-input) */
+#define NA_COL(a, b, c, d, k)                                                            \
+    xor3(xor3(L.te[0][(a) >> 24], L.te[1][((b) >> 16) & 255], L.te[2][((c) >> 8) & 255]), \
+         L.te[3][(d) & 255], rk[k])
+        const uint32_t t0 = NA_COL(s0, s1, s2, s3, 4 * r);
+        const uint32_t t1 = NA_COL(s1, s2, s3, s0, 4 * r + 1);
+        const uint32_t t2 = NA_COL(s2, s3, s0, s1, 4 * r + 2);
+        const uint32_t t3 = NA_COL(s3, s0, s1, s2, 4 * r + 3);
+#undef NA_COL
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     /* last round: S-box bytes picked out of the T-tables (Te0 = [2s,s,s,3s]) */
@@ -439,7 +459,7 @@ __global__ __launch_bounds__(256) void gcm_staged(UniformArgs a)
     /* GHASH (and, sealing, CTR) over this lane's blocks i = c0, c0+K, ... */
     uint32_t acc[4] = {0, 0, 0, 0};
     for (uint32_t i = c0; i < n; i += K) {
-        if (i != c0) gh_mul(acc, L.h4);
+        if (i != c0) gh_mul_lds(acc, L.h4);
         uint32_t x[4];
         if (i >= A && i < A + M) {
             const uint32_t d = i - A;

@@ -9,7 +9,11 @@ timeout -k 10 300 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { tai
 cat $O/bench_c2.json
 timeout -k 10 200 python bench.py --config c3 --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err || { tail -20 $O/bench_c3.err; exit 1; }
 timeout -k 10 200 python bench.py --config c4 --no-cpu-baseline --steps 20 > $O/bench_c4.json 2> $O/bench_c4.err || { tail -20 $O/bench_c4.err; exit 1; }
-cat $O/bench_c3.json $O/bench_c4.json
+timeout -k 10 300 python bench.py --config c5 --no-cpu-baseline --steps 10 --warmup 2 --verify > $O/bench_c5.json 2> $O/bench_c5.err || { tail -20 $O/bench_c5.err; exit 1; }
+cat $O/bench_c3.json $O/bench_c4.json $O/bench_c5.json
+timeout -k 10 300 python tools/e2e.py > $O/e2e_c2.json 2> $O/e2e_c2.err || { tail -20 $O/e2e_c2.err; exit 1; }
+timeout -k 10 300 python tools/e2e.py --cipher aesgcm > $O/e2e_c3.json 2> $O/e2e_c3.err || { tail -20 $O/e2e_c3.err; exit 1; }
+cat $O/e2e_c2.json $O/e2e_c3.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline > $O/prof_c2.log 2>&1 || { tail -20 $O/prof_c2.log; exit 1; }
 cd $R
