@@ -168,11 +168,16 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
             return NOISE_ERROR_INVALID_PARAM;
         rc = hip_rc(ensure_aes_tables(s));
         if (rc) return rc;
-        /* one state per 64-record workgroup + FAST layout -> LDS-staged kernel */
-        const bool staged = uniform_fast(job, open) && job->recs_per_state % 64 == 0;
-        KernelFn<UniformArgs> fn = staged ? (open ? gcm_staged<true> : gcm_staged<false>)
-                                          : (open ? gcm_uniform<true> : gcm_uniform<false>);
-        return launch(fn, job->n_records, GCM_LANES, a, s);
+        /* one state per 256-record workgroup + FAST layout -> LDS-staged kernel */
+        if (uniform_fast(job, open) && job->recs_per_state % GCM_WG_RECS == 0) {
+            if (job->n_records == 0) return NOISE_ERROR_NONE;
+            const uint32_t blocks = (job->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
+            hipLaunchKernelGGL(open ? gcm_staged<true> : gcm_staged<false>, dim3(blocks),
+                               dim3(GCM_WG), 0, s, a);
+            return hip_rc(hipGetLastError());
+        }
+        return launch(open ? gcm_uniform<true> : gcm_uniform<false>, job->n_records,
+                      GCM_LANES, a, s);
     }
     return NOISE_ERROR_UNKNOWN_ID;
 }

@@ -122,6 +122,7 @@ NA_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdg
 
 /* gh_mul with the table in LDS: lookups taken in pairs so every accumulate is
    one 3-input XOR */
+template <bool THROTTLE = false>
 NA_DEV void gh_mul_lds(uint32_t y[4], const uint4 *tab)
 {
     uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
@@ -133,6 +134,9 @@ NA_DEV void gh_mul_lds(uint32_t y[4], const uint4 *tab)
         const uint4 f = tab[(p + 1) * 16 + (byte & 15)];
         r0 = xor3(r0, e.x, f.x); r1 = xor3(r1, e.y, f.y);
         r2 = xor3(r2, e.z, f.z); r3 = xor3(r3, e.w, f.w);
+        /* THROTTLE: at most 8 table rows (32 VGPRs) in flight, where hipcc
+           would otherwise hoist all 32 reads of an unrolled GHASH-only loop */
+        if (THROTTLE && (p & 6) == 6) asm volatile("" ::: "memory");
     }
     y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
 }
@@ -365,18 +369,27 @@ __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
     if (OPEN && l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
-/* ------------------------------------- staged (uniform FAST, one state per WG)
+/* ---------------------------- staged (uniform FAST, one state per workgroup)
  *
- * For uniform batches whose 64 records per workgroup share one CipherState
- * (recs_per_state a multiple of 64) and FAST layouts.  The workgroup copies
- * into LDS once: the four T-tables Te0..Te3 (no rotates in the rounds), the
- * state's round keys, and its multiply-by-H^4 GHASH table (the Horner step),
- * so the per-block work touches no global memory but the record bytes.  The
- * record's data blocks are 16-B aligned dwordx4 loads/stores; the input is
- * loaded at the top of each step and consumed after the AES block.
+ * For uniform batches whose 256 records per workgroup share one CipherState
+ * (recs_per_state a multiple of 256) and FAST layouts.  1024-thread
+ * workgroups (one per CU, 4 waves per SIMD) hold in LDS:
+ *  - the four AES T-tables, each replicated 32x so that lane c (mod 32) of a
+ *    ds_read_b32 lane group always hits bank c: conflict-free lookups (the
+ *    b32 reads bank on (a/4) mod 32, MI355X_MICROARCH.md §LDS).  Row i of a
+ *    table is 128 B (32 copies of Te_t[i]); Te0|Te1 rows interleave in the
+ *    first 64 KB (row stride 256 B), Te2|Te3 in the second.  The lookup
+ *    address (t>=2)<<16 | byte<<8 | (t&1)<<7 | 4c is one v_perm_b32 of the
+ *    state word and a per-lane template word;
+ *  - the state's round keys and its multiply-by-H^4 GHASH table (16 entries
+ *    x 16 B per nibble position: a 16-lane b128 group is conflict-free).
+ * The per-block work then touches no global memory but the record bytes.
  */
+constexpr int GCM_WG = 1024;                  /* threads per staged workgroup */
+constexpr int GCM_WG_RECS = GCM_WG / GCM_LANES;
+
 struct GcmLds {
-    uint32_t te[4][256]; /* te[k][x] = rotr(Te0[x], 8k) */
+    uint32_t te[2][256][64]; /* [Te0|Te1 or Te2|Te3][row][32 + 32 copies] */
     uint4 h4[GHASH_TAB_ENTRIES];
     uint32_t rk[60];
 };
@@ -384,24 +397,42 @@ struct GcmLds {
 NA_DEV void gcm_lds_fill(GcmLds &L, const AesCtx *ctx)
 {
     const int t = threadIdx.x;
-    const uint32_t e = g_te0[t];
-    L.te[0][t] = e; L.te[1][t] = rotr(e, 8); L.te[2][t] = rotr(e, 16); L.te[3][t] = rotr(e, 24);
+    /* 2 regions x 256 rows x 64 words = 32768 words: 8 uint4 per thread */
+    for (int q = t; q < 2 * 256 * 16; q += GCM_WG) {
+        const int reg = q >> 12, row = (q >> 4) & 255, quad = q & 15;
+        const int tab = 2 * reg + (quad >> 3); /* words 0-31: Te(2reg), 32-63: Te(2reg+1) */
+        const uint32_t v = rotr(g_te0[row], 8 * tab);
+        ((uint4 *)&L.te[reg][row][0])[quad] = make_uint4(v, v, v, v);
+    }
     const uint4 *src = (const uint4 *)ctx->tab[GCM_LANES - 1];
-    for (int i = t; i < GHASH_TAB_ENTRIES; i += 256) L.h4[i] = src[i];
+    for (int i = t; i < GHASH_TAB_ENTRIES; i += GCM_WG) L.h4[i] = src[i];
     if (t < 60) L.rk[t] = ctx->rk[t];
     __syncthreads();
 }
 
-NA_DEV void aes256_lds(const GcmLds &L, uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3)
+template <int TAB, int K>
+NA_DEV uint32_t te_lookup(const GcmLds &L, uint32_t s, uint32_t lane_tpl)
+{
+    /* perm: out byte0 = tpl byte0 (4c) or byte1 (128 + 4c) for Te1/Te3,
+       byte1 = s byte K, byte2 = tpl byte2 (1) for Te2/Te3 else 0, byte3 = 0 */
+    constexpr uint32_t sel = (0x0cu << 24) | ((TAB >= 2 ? 2u : 0x0cu) << 16) | ((4u + K) << 8) |
+                             (TAB & 1 ? 1u : 0u);
+    const uint32_t addr = __builtin_amdgcn_perm(s, lane_tpl, sel);
+    return *(const uint32_t *)((const uint8_t *)&L.te[0][0][0] + addr);
+}
+
+NA_DEV void aes256_lds(const GcmLds &L, uint32_t tpl, uint32_t &s0, uint32_t &s1, uint32_t &s2,
+                       uint32_t &s3)
 {
     const uint32_t *rk = L.rk;
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
-        /* 5-input XOR as two v_bitop3 (3-input) */
-#define NA_COL(a, b, c, d, k)                                                            \
-    xor3(xor3(L.te[0][(a) >> 24], L.te[1][((b) >> 16) & 255], L.te[2][((c) >> 8) & 255]), \
-         L.te[3][(d) & 255], rk[k])
+        /* Te0[a>>24] ^ Te1[(b>>16)&255] ^ Te2[(c>>8)&255] ^ Te3[d&255] ^ rk */
+#define NA_COL(a, b, c, d, k)                                                        \
+    xor3(xor3(te_lookup<0, 3>(L, a, tpl), te_lookup<1, 2>(L, b, tpl),                   \
+              te_lookup<2, 1>(L, c, tpl)),                                             \
+         te_lookup<3, 0>(L, d, tpl), rk[k])
         const uint32_t t0 = NA_COL(s0, s1, s2, s3, 4 * r);
         const uint32_t t1 = NA_COL(s1, s2, s3, s0, 4 * r + 1);
         const uint32_t t2 = NA_COL(s2, s3, s0, s1, 4 * r + 2);
@@ -409,20 +440,22 @@ NA_DEV void aes256_lds(const GcmLds &L, uint32_t &s0, uint32_t &s1, uint32_t &s2
 #undef NA_COL
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-    /* last round: S-box bytes picked out of the T-tables (Te0 = [2s,s,s,3s]) */
-#define NA_SB4(a, b, c, d)                                                        \
-    ((L.te[2][(a) >> 24] & 0xff000000u) | (L.te[3][((b) >> 16) & 255] & 0x00ff0000u) | \
-     (L.te[0][((c) >> 8) & 255] & 0x0000ff00u) | (L.te[1][(d) & 255] & 0x000000ffu))
+    /* last round: S-box bytes out of the T-tables (Te0 = [2s,s,s,3s] MSB first,
+       Te1 = [3s,2s,s,s], Te2 = [s,3s,2s,s], Te3 = [s,s,3s,2s]) */
+#define NA_SB4(a, b, c, d)                                                          \
+    ((te_lookup<2, 3>(L, a, tpl) & 0xff000000u) | (te_lookup<3, 2>(L, b, tpl) & 0x00ff0000u) | \
+     (te_lookup<0, 1>(L, c, tpl) & 0x0000ff00u) | (te_lookup<1, 0>(L, d, tpl) & 0x000000ffu))
     const uint32_t o0 = NA_SB4(s0, s1, s2, s3), o1 = NA_SB4(s1, s2, s3, s0);
     const uint32_t o2 = NA_SB4(s2, s3, s0, s1), o3 = NA_SB4(s3, s0, s1, s2);
 #undef NA_SB4
     s0 = o0 ^ rk[56]; s1 = o1 ^ rk[57]; s2 = o2 ^ rk[58]; s3 = o3 ^ rk[59];
 }
 
-NA_DEV void aes_ctr_lds(const GcmLds &L, uint32_t n_hi, uint32_t n_lo, uint32_t ctr, uint32_t ks[4])
+NA_DEV void aes_ctr_lds(const GcmLds &L, uint32_t tpl, uint32_t n_hi, uint32_t n_lo, uint32_t ctr,
+                        uint32_t ks[4])
 {
     uint32_t s0 = 0, s1 = n_hi, s2 = n_lo, s3 = ctr;
-    aes256_lds(L, s0, s1, s2, s3);
+    aes256_lds(L, tpl, s0, s1, s2, s3);
     ks[0] = __builtin_bswap32(s0); ks[1] = __builtin_bswap32(s1);
     ks[2] = __builtin_bswap32(s2); ks[3] = __builtin_bswap32(s3);
 }
@@ -435,17 +468,21 @@ NA_DEV uint32_t blk_mask(uint32_t nb, int w)
 }
 
 template <bool OPEN>
-__global__ __launch_bounds__(256) void gcm_staged(UniformArgs a)
+__global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
 {
     constexpr int K = GCM_LANES;
     __shared__ GcmLds L;
-    const uint32_t rec0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (256u / K));
+    const uint32_t rec0 = blockIdx.x * (uint32_t)GCM_WG_RECS;
     const uint32_t st = rec0 / a.rps; /* one state per workgroup (host-checked) */
     const AesCtx *ctx = (const AesCtx *)a.keys + st;
     gcm_lds_fill(L, ctx);
 
     const uint32_t rec = rec0 + threadIdx.x / K;
     if (rec >= a.n_records) return;
+    const uint32_t lane = threadIdx.x & 63;
+    /* lookup template: byte0 = 4c (Te0/Te2 copy c = lane mod 32), byte1 =
+       128 + 4c (Te1/Te3), byte2 = 1 (the Te2|Te3 region at 64 KB) */
+    const uint32_t tpl = (1u << 16) | ((128u + 4u * (lane & 31)) << 8) | (4u * (lane & 31));
     const int l = (int)(threadIdx.x % K);
     const uint64_t nonce = a.nonce_base[st] + (uint64_t)(rec - st * a.rps);
     const uint32_t n_hi = (uint32_t)(nonce >> 32), n_lo = (uint32_t)nonce;
@@ -458,8 +495,9 @@ __global__ __launch_bounds__(256) void gcm_staged(UniformArgs a)
 
     /* GHASH (and, sealing, CTR) over this lane's blocks i = c0, c0+K, ... */
     uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll 1
     for (uint32_t i = c0; i < n; i += K) {
-        if (i != c0) gh_mul_lds(acc, L.h4);
+        if (i != c0) gh_mul_lds<OPEN>(acc, L.h4);
         uint32_t x[4];
         if (i >= A && i < A + M) {
             const uint32_t d = i - A;
@@ -468,7 +506,7 @@ __global__ __launch_bounds__(256) void gcm_staged(UniformArgs a)
             const uint32_t nb = min(len - 16 * d, 16u);
             if (!OPEN) {
                 uint32_t ks[4];
-                aes_ctr_lds(L, n_hi, n_lo, 2 + d, ks);
+                aes_ctr_lds(L, tpl, n_hi, n_lo, 2 + d, ks);
 #pragma unroll
                 for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
                 if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
@@ -486,14 +524,14 @@ __global__ __launch_bounds__(256) void gcm_staged(UniformArgs a)
         }
         acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
     }
-    /* scale by H^(K-l): lane K-1 by H, from the context's tables (once) */
+    /* scale by H^(K-l) from the context's tables (once per lane) */
     gh_mul(acc, (const uint4 *)ctx->tab[K - 1 - l]);
 #pragma unroll
     for (int off = 1; off < K; off <<= 1)
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
     uint32_t ej[4];
-    aes_ctr_lds(L, n_hi, n_lo, 1u, ej);
+    aes_ctr_lds(L, tpl, n_hi, n_lo, 1u, ej);
     const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
     if (!OPEN) {
         if (l == K - 1) {
@@ -513,7 +551,7 @@ __global__ __launch_bounds__(256) void gcm_staged(UniformArgs a)
     for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
         const uint4 v = *(const uint4 *)(src + 16 * d);
         uint32_t x[4] = {v.x, v.y, v.z, v.w}, ks[4];
-        aes_ctr_lds(L, n_hi, n_lo, 2 + d, ks);
+        aes_ctr_lds(L, tpl, n_hi, n_lo, 2 + d, ks);
 #pragma unroll
         for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
         const uint32_t nb = min(len - 16 * d, 16u);

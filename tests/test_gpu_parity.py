@@ -142,6 +142,43 @@ def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed, r
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L])
 
 
+@pytest.mark.parametrize("cipher", [CHACHA, AES])
+def test_uniform_staged_kernels(aead, gpu, oracle, cipher):
+    """FAST layouts with one state per 256 records: the LDS-staged kernels
+    (ChaChaPoly wave-uniform key, AESGCM replicated T-tables) on a batch whose
+    last workgroup is partial, every record vs the oracle, with AD."""
+    rng = np.random.default_rng(4242 + (cipher & 3))
+    rps, count = 256, 600
+    S = (count + rps - 1) // rps
+    for L, adl in [(0, 0), (1, 0), (15, 0), (16, 0), (17, 0), (100, 0), (1400, 0), (1401, 0),
+                   (4096, 0), (1400, 13), (64, 32)]:
+        keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
+        nb = rng.integers(0, 2**62, S, dtype=np.uint64)
+        in_stride = (max(L, 1) + 63) // 64 * 64
+        out_stride = (L + 16 + 63) // 64 * 64
+        pt = rng.integers(0, 256, count * in_stride + 64, dtype=np.uint8)
+        ad = rng.integers(0, 256, count * 48 + 64, dtype=np.uint8)
+        kw = dict(ad=ad, ad_stride=48, ad_len=adl) if adl else {}
+        exp = oracle_seal_records(oracle, cipher, keys, nb, rps, pt, in_stride, L, count,
+                                  out_stride, **kw)
+        got, _ = gpu_uniform(aead, False, cipher, keys, nb, rps, pt, in_stride, L, count,
+                             out_stride, **kw)
+        assert np.array_equal(got[:count * out_stride], exp[:count * out_stride]), f"len={L} ad={adl}"
+        ct = got.copy()
+        bad = sorted(set(int(x) for x in rng.integers(0, count, 7)))
+        for b in bad:
+            ct[b * out_stride + int(rng.integers(0, L + 16))] ^= 0x80
+        back, st = gpu_uniform(aead, True, cipher, keys, nb, rps, ct, out_stride, L, count,
+                               in_stride, out_init=0x3C, **kw)
+        for i in range(count):
+            seg = back[i * in_stride: i * in_stride + L]
+            if i in bad:
+                assert st[i] == 1 and np.all(seg == 0x3C), f"len={L} rec={i}"
+            else:
+                assert st[i] == 0, f"len={L} rec={i}"
+                assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L]), f"len={L} rec={i}"
+
+
 @pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 4), (CHACHA, 8), (AES, 0)])
 @pytest.mark.parametrize("rps", [4, 16])
 def test_uniform_with_ad(aead, gpu, oracle, cipher, lanes, rps):
