@@ -142,6 +142,17 @@ def cpu_baseline(cfg, budget_cpu_s: float = 12.0):
             "ok": r["ok"]}
 
 
+def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length):
+    """The seal kernel the library dispatches for this uniform job
+    (aead_api.hip run_uniform), as rocprofv3 names it."""
+    fast = in_stride % 16 == 0 and out_stride % 16 == 0 and in_stride >= (max(length, 1) + 63) // 64 * 64
+    if cipher == AES:
+        return "gcm_staged<false>" if fast and rps % 256 == 0 else "gcm_uniform<false>"
+    if fast and lanes >= 4:
+        return f"chachapoly_seal_staged<{lanes}, {'true' if rps % (64 // lanes) == 0 else 'false'}>"
+    return f"chachapoly_seal_uniform<{lanes}, {'true' if fast else 'false'}>"
+
+
 def load_traffic(config_name: str, kernel: str):
     path = os.path.join(ROOT, "profiles", f"traffic_{config_name}.json")
     if not os.path.exists(path):
@@ -268,7 +279,7 @@ def main():
     value = payload_step * args.steps / elapsed / GIB
     alg_seal = N * (2 * L + 16) + len(sh["key_ids"]) * 40       # SURVEY §8d algorithmic bytes
     achieved = alg_seal / (seal_ms * 1e-3) / 1e9
-    kname = "chachapoly_seal_uniform" if cipher == CHACHA else "gcm_uniform<false>"
+    kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L)
     traffic = load_traffic(args.config, kname)
     result = {
         "metric": "GiB/s device-resident AEAD encrypt+decrypt, 64Ki x 1400B records per GPU",

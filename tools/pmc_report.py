@@ -15,14 +15,10 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for key in ("chachapoly_seal_uniform", "chachapoly_open_uniform", "gcm_uniform<false>",
-                "gcm_uniform<true>", "chachapoly_seal_ragged", "chachapoly_open_ragged"):
-        base = key.split("<")[0]
-        if base in name:
-            if key.startswith("gcm"):
-                return "gcm_uniform<true>" if "<true>" in name or "ILb1E" in name else "gcm_uniform<false>"
-            return key
-    return name
+    """Kernel name without namespace/arguments, template args kept:
+    'void na::gcm_staged<false>(na::UniformArgs)' -> 'gcm_staged<false>'."""
+    n = name.split("(")[0].replace("void ", "").replace("na::", "").strip()
+    return n
 
 
 def load(d):
