@@ -173,6 +173,9 @@ def main():
     ap.add_argument("--sets", type=int, default=4, help="rotating batch sets (> MALL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check every open status after timing")
+    ap.add_argument("--no-xfer", action="store_true",
+                    help="skip the N>1 scatter/seal/gather leg (RCCL, SURVEY.md 8e)")
+    ap.add_argument("--xfer-reps", type=int, default=5)
     args = ap.parse_args()
 
     import torch
@@ -222,8 +225,9 @@ def main():
 
     lanes = args.lanes or A.dev_default_lanes(cipher, N)
 
-    def seal(b):
-        pt, ct, _, _ = sets[b]
+    def seal(b, pt=None, ct=None):
+        if pt is None:
+            pt, ct, _, _ = sets[b]
         return A.dev_uniform(False, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
                              inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
                              out_stride=out_stride, length=L, n_records=N,
@@ -309,6 +313,12 @@ def main():
     }
     if args.verify:
         result["verified"] = ok
+    if world > 1 and not args.no_xfer:
+        try:  # reported beside the value; a failure here never voids the bench line
+            result["scatter_gather"] = xfer_leg(args, torch, dist, dev, A, rank, world, N, L,
+                                                in_stride, out_stride, sh, sets, seal)
+        except Exception as e:
+            result["scatter_gather"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(cfg)
@@ -318,6 +328,66 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def xfer_leg(args, torch, dist, dev, A, rank, world, N, L, in_stride, out_stride, sh, sets, seal):
+    """the batch starts and ends on rank 0's GPU.  Rank 0 holds
+    the whole job's plaintext (world shards, each equal to that rank's set-0
+    input), RCCL scatters the shards, every rank seals its own, RCCL gathers
+    the sealed shards back to rank 0.  Timed per phase (max over ranks);
+    reported beside, never instead of, the device-resident value."""
+    from distribute import scatter_records, gather_records
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    shard_in, shard_out = N * in_stride, N * out_stride
+    full_in = full_out = None
+    if rank == 0:
+        full_in = torch.empty(world * shard_in, dtype=torch.uint8, device=dev)
+        full_out = torch.empty(world * shard_out, dtype=torch.uint8, device=dev)
+        for g in range(world):  # shard g = rank g's set-0 plaintext (same SplitMix64 words)
+            assert A.dev_fill_splitmix(full_in[g * shard_in:].data_ptr(), shard_in, 0x7074,
+                                       (g * N * in_stride) // 8, sp) == 0
+    local_in = torch.empty(shard_in, dtype=torch.uint8, device=dev)
+    local_out = torch.empty(shard_out, dtype=torch.uint8, device=dev)
+    phases = []
+    for rep in range(args.xfer_reps + 1):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        scatter_records(local_in, full_in, src=0)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        if seal(0, local_in, local_out):
+            raise RuntimeError("seal launch failed")
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        gather_records(local_out, full_out, dst=0)
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        if rep:  # rep 0 warms RCCL's channels
+            phases.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0))
+    ph = torch.tensor(phases, dtype=torch.float64, device=dev).mean(0)
+    dist.all_reduce(ph, op=dist.ReduceOp.MAX)
+    # checks: scattered shard == this rank's own input; gathered shard g ==
+    # rank g's sealed output (int64 checksums, all_gathered)
+    ok = torch.tensor([1 if torch.equal(local_in, sets[0][0]) else 0], device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    mine = local_out.view(torch.int64).sum().reshape(1)
+    sums = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(sums, mine)
+    good = bool(ok.item())
+    if rank == 0:
+        for g in range(world):
+            got = full_out[g * shard_out:(g + 1) * shard_out].view(torch.int64).sum()
+            good &= bool(got.item() == sums[g].item())
+    sc, se, ga, tot = (float(x) * 1e3 for x in ph.tolist())
+    return {"collective": "torch.distributed scatter/gather on nccl (RCCL grouped send/recv over xGMI)",
+            "src_dst_rank": 0, "shard_in_bytes": shard_in, "shard_out_bytes": shard_out,
+            "scatter_ms": round(sc, 4), "seal_ms": round(se, 4), "gather_ms": round(ga, 4),
+            "total_ms": round(tot, 4),
+            "seal_gibs_incl_xfer": round(N * L * world / (tot * 1e-3) / GIB, 2),
+            "scatter_gbs": round((world - 1) * shard_in / (sc * 1e-3) / 1e9, 1),
+            "gather_gbs": round((world - 1) * shard_out / (ga * 1e-3) / 1e9, 1),
+            "verified": good, "reps": args.xfer_reps}
 
 
 def run_mixed(args, cfg, A, torch, dev, rank, world, dist):

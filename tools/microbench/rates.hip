@@ -26,6 +26,20 @@ K(k_perm, X8_3("v_perm_b32"))
 K(k_mullo, X8("v_mul_lo_u32"))
 K(k_mul24, X8("v_mul_u32_u24"))
 K(k_bitop3, "v_bitop3_b32 %0, %0, %8, %0 bitop3:0x96\n" "v_bitop3_b32 %1, %1, %8, %1 bitop3:0x96\n" "v_bitop3_b32 %2, %2, %8, %2 bitop3:0x96\n" "v_bitop3_b32 %3, %3, %8, %3 bitop3:0x96\n" "v_bitop3_b32 %4, %4, %8, %4 bitop3:0x96\n" "v_bitop3_b32 %5, %5, %8, %5 bitop3:0x96\n" "v_bitop3_b32 %6, %6, %8, %6 bitop3:0x96\n" "v_bitop3_b32 %7, %7, %8, %7 bitop3:0x96\n")
+
+K(k_sdwa, "v_xor_b32_sdwa %0, %0, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n" "v_xor_b32_sdwa %1, %1, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n" "v_xor_b32_sdwa %2, %2, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n" "v_xor_b32_sdwa %3, %3, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n" "v_xor_b32_sdwa %4, %4, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n" "v_xor_b32_sdwa %5, %5, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n" "v_xor_b32_sdwa %6, %6, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n" "v_xor_b32_sdwa %7, %7, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n")
+K(k_lshl, X8("v_lshlrev_b32"))
+K(k_lshlor, X8_3("v_lshl_or_b32"))
+K(k_lshladd, X8_3("v_lshl_add_u32"))
+K(k_xad, X8_3("v_xad_u32"))
+K(k_andor, X8_3("v_and_or_b32"))
+K(k_or3, X8_3("v_or3_b32"))
+K(k_bfe, X8_3("v_bfe_u32"))
+K(k_alignbyte, X8_3("v_alignbyte_b32"))
+K(k_and, X8("v_and_b32"))
+K(k_xor_e64, X8("v_xor_b32_e64"))
+K(k_mix_xa, "v_xor_b32 %0, %0, %8\n v_alignbit_b32 %1, %1, %1, 7\n v_xor_b32 %2, %2, %8\n v_alignbit_b32 %3, %3, %3, 7\n v_xor_b32 %4, %4, %8\n v_alignbit_b32 %5, %5, %5, 7\n v_xor_b32 %6, %6, %8\n v_alignbit_b32 %7, %7, %7, 7\n")
+K(k_mix_xxa, "v_xor_b32 %0, %0, %8\n v_add_u32 %1, %1, %8\n v_alignbit_b32 %2, %2, %2, 7\n v_xor_b32 %3, %3, %8\n v_add_u32 %4, %4, %8\n v_alignbit_b32 %5, %5, %5, 7\n v_xor_b32 %6, %6, %8\n v_add_u32 %7, %7, %8\n")
 // packed fp32 add on register pairs: a0:a1 ... 4 instr per body line
 __global__ void __launch_bounds__(256) k_pkadd(uint32_t *o, uint32_t s) {
   float a[8]; for (int i=0;i<8;++i) a[i]=s+threadIdx.x*i;
@@ -93,6 +107,10 @@ int main() {
   };
   run(k_xor,"v_xor_b32",32); run(k_add,"v_add_u32",32); run(k_addf,"v_add_f32",32); run(k_align,"v_alignbit",32);
   run(k_add3,"v_add3_u32",32); run(k_perm,"v_perm_b32",32); run(k_bitop3,"v_bitop3_b32",32); run(k_mullo,"v_mul_lo_u32",32);
-  run(k_mul24,"v_mul_u32_u24",32); run(k_pkadd,"v_pk_add_f32",32); run(k_mad64,"v_mad_u64_u32",32); run(k_shr64,"v_lshrrev_b64",32);
+  run(k_mul24,"v_mul_u32_u24",32);
+  run(k_sdwa,"v_xor_sdwa",32); run(k_lshl,"v_lshlrev_b32",32); run(k_lshlor,"v_lshl_or_b32",32); run(k_lshladd,"v_lshl_add_u32",32);
+  run(k_xad,"v_xad_u32",32); run(k_andor,"v_and_or_b32",32); run(k_or3,"v_or3_b32",32); run(k_bfe,"v_bfe_u32",32);
+  run(k_alignbyte,"v_alignbyte",32); run(k_and,"v_and_b32",32); run(k_xor_e64,"v_xor_b32_e64",32);
+  run(k_mix_xa,"mix xor/align",32); run(k_mix_xxa,"mix xor/add/al",32); run(k_pkadd,"v_pk_add_f32",32); run(k_mad64,"v_mad_u64_u32",32); run(k_shr64,"v_lshrrev_b64",32);
   return 0;
 }
