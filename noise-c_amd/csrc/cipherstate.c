@@ -9,12 +9,16 @@
  * no cryptographic arithmetic at all — it validates, assigns nonces, stages
  * bytes and launches.
  */
+#define _DEFAULT_SOURCE
 #include "noise_aead_hip.h"
+#include "host_pool.h"
 
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
+#include <time.h>
 
 /* ------------------------------------------------- the plugin object ABI */
 
@@ -77,13 +81,22 @@ static void free_object(void *ptr, size_t size) /* util.c:152-158 noise_free */
 
 /* ------------------------------------------------------ per-thread staging */
 
+/* The batch path moves records through one pinned host area and one device
+   area per thread, cut into chunks that form a pipeline:
+     host threads pack chunk c+1 while chunk c crosses PCIe (copy-in stream)
+     and runs on the GPU, and the host unpacks chunk c-1 as its D2H lands.
+   H2D and D2H use different streams, so both PCIe directions are busy. */
+#define MAX_CHUNKS 64
+#define CHUNK_MIN ((size_t)4 << 20)
+
 typedef struct {
     int device;
-    hipStream_t stream;
+    hipStream_t stream;    /* kernels + D2H */
+    hipStream_t stream_in; /* H2D */
+    hipEvent_t ev_in[MAX_CHUNKS], ev_out[MAX_CHUNKS];
     uint8_t *h;        /* pinned host */
     uint8_t *d;        /* device */
     size_t cap;
-    size_t scrub_off, scrub_len; /* last payload range (plaintext) */
 } Staging;
 
 static pthread_key_t g_stage_key;
@@ -95,7 +108,12 @@ static void stage_destroy(void *p)
     if (!s) return;
     if (s->h) (void)hipHostFree(s->h);
     if (s->d) (void)hipFree(s->d);
+    for (int i = 0; i < MAX_CHUNKS; ++i) {
+        if (s->ev_in[i]) (void)hipEventDestroy(s->ev_in[i]);
+        if (s->ev_out[i]) (void)hipEventDestroy(s->ev_out[i]);
+    }
     if (s->stream) (void)hipStreamDestroy(s->stream);
+    if (s->stream_in) (void)hipStreamDestroy(s->stream_in);
     free(s);
 }
 
@@ -117,8 +135,13 @@ static Staging *stage_get(size_t bytes)
         s = (Staging *)calloc(1, sizeof(Staging));
         if (!s) return NULL;
         s->device = dev;
-        if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
-            free(s);
+        int ok = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess &&
+                 hipStreamCreateWithFlags(&s->stream_in, hipStreamNonBlocking) == hipSuccess;
+        for (int i = 0; ok && i < MAX_CHUNKS; ++i)
+            ok = hipEventCreateWithFlags(&s->ev_in[i], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&s->ev_out[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            stage_destroy(s);
             return NULL;
         }
         pthread_setspecific(g_stage_key, s);
@@ -136,16 +159,6 @@ static Staging *stage_get(size_t bytes)
         s->cap = cap;
     }
     return s;
-}
-
-/* Zero the last payload staged on this thread: no plaintext left behind
-   (the reference cleans its scratch the same way, cipher-chachapoly.c:72). */
-static void stage_scrub(void)
-{
-    pthread_once(&g_stage_once, stage_key_init);
-    Staging *s = (Staging *)pthread_getspecific(g_stage_key);
-    if (s && s->h && s->scrub_len) clean(s->h + s->scrub_off, s->scrub_len);
-    if (s) s->scrub_len = 0;
 }
 
 /* --------------------------------------------------- device key contexts */
@@ -193,10 +206,24 @@ typedef struct {
     uint8_t *data;     /* record; tag at data + len */
     size_t len;        /* plaintext (seal) / ciphertext-without-tag (open) */
     uint64_t nonce;
+    size_t idx;        /* caller's record index */
+    int skip;          /* in: not dispatched (nonce exhausted) */
     int status;        /* out: NOISE_ERROR_NONE / _MAC_FAILURE / _SYSTEM */
-    const uint8_t *result; /* out (open): verified plaintext in staging, valid
-                              until the next run_jobs / stage_scrub */
+    int commit;        /* set by the decide step: copy the result to data */
+    int defer;         /* set by the decide step: retry in a later round */
+    size_t off, ad_off; /* staging offsets of the record slot and its AD */
+    uint32_t desc;     /* descriptor index within its chunk */
 } Job;
+
+/* Decide, in record order, which finished jobs of [lo, hi) commit.  Called
+   once per chunk, chunks in order, so every earlier record's fate is known. */
+typedef void (*decide_fn)(Job *jobs, size_t lo, size_t hi, void *u);
+
+typedef struct {
+    size_t j0, j1;              /* jobs [j0, j1) */
+    size_t recs_off, status_off, payload_off, end;
+    uint32_t n_chacha, n_aes;
+} Chunk;
 
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -208,111 +235,260 @@ static size_t slot_bytes(size_t len)
     return a > b ? a : b;
 }
 
-/* Run a set of jobs (any mix of states and ciphers) in one staging round
-   trip: pack records into pinned memory, one H2D, one ragged kernel per
-   cipher, one D2H.  Fills job.status.  Seal results are copied back at once;
-   open results stay in staging (job.result) until the caller commits them
-   in record order and calls stage_scrub() — a record verified under a
-   speculative nonce must not touch the caller's buffer. */
-static int run_jobs(Job *jobs, size_t n, int open)
+static size_t job_bytes(const Job *j)
 {
-    if (n == 0) return NOISE_ERROR_NONE;
-    /* layout: [recs: n x 48][status: n][payload...] */
-    size_t off = align16(n * sizeof(NoiseAeadRecord));
-    const size_t status_off = off;
-    off = align16(off + n);
-    const size_t payload_off = off;
-    for (size_t i = 0; i < n; ++i) off += align16(jobs[i].ad_len) + slot_bytes(jobs[i].len);
-    const size_t total = off + 64;
-    Staging *sg = stage_get(total);
-    if (!sg) {
-        for (size_t i = 0; i < n; ++i) jobs[i].status = NOISE_ERROR_SYSTEM;
-        return NOISE_ERROR_SYSTEM;
-    }
-    int rc = NOISE_ERROR_NONE;
-    for (size_t i = 0; i < n && !rc; ++i) rc = ensure_ctx(jobs[i].st, sg);
-    if (rc) {
-        for (size_t i = 0; i < n; ++i) jobs[i].status = NOISE_ERROR_SYSTEM;
-        return rc;
-    }
+    return j->skip ? 0 : sizeof(NoiseAeadRecord) + 1 + align16(j->ad_len) + slot_bytes(j->len);
+}
 
-    /* ChaChaPoly records first, then AESGCM, so each cipher's descriptors
-       are contiguous */
-    NoiseAeadRecord *recs = (NoiseAeadRecord *)sg->h;
-    size_t *order = (size_t *)malloc(n * sizeof(size_t));
-    if (!order) {
-        for (size_t i = 0; i < n; ++i) jobs[i].status = NOISE_ERROR_NO_MEMORY;
-        return NOISE_ERROR_NO_MEMORY;
+typedef struct {
+    Job *jobs;
+    uint8_t *h;
+    int open;
+    size_t base;   /* byte range for the scrub step */
+} CopyArg;
+
+static void pack_range(void *p, size_t lo, size_t hi)
+{
+    CopyArg *a = (CopyArg *)p;
+    for (size_t k = lo; k < hi; ++k) {
+        const Job *j = &a->jobs[k];
+        if (j->skip) continue;
+        if (j->ad_len) memcpy(a->h + j->ad_off, j->ad, j->ad_len);
+        memcpy(a->h + j->off, j->data, j->len + (a->open ? 16 : 0));
     }
-    size_t n_chacha = 0, slot = 0;
+}
+
+static void unpack_range(void *p, size_t lo, size_t hi)
+{
+    CopyArg *a = (CopyArg *)p;
+    for (size_t k = lo; k < hi; ++k) {
+        const Job *j = &a->jobs[k];
+        if (j->commit) memcpy(j->data, a->h + j->off, j->len + (a->open ? 0 : 16));
+    }
+}
+
+static void scrub_range(void *p, size_t lo, size_t hi)
+{
+    CopyArg *a = (CopyArg *)p;
+    explicit_bzero(a->h + a->base + lo, hi - lo);
+}
+
+static size_t copy_grain(const Chunk *c, size_t n)
+{
+    size_t per = (c->end - c->payload_off) / (n ? n : 1) + 1;
+    size_t g = ((size_t)256 << 10) / per;
+    return g ? g : 1;
+}
+
+/* Plan chunk c's staging layout starting at byte `at`; returns its end. */
+static size_t plan_chunk(Job *jobs, Chunk *c, size_t at)
+{
+    size_t nd = 0;
+    for (size_t k = c->j0; k < c->j1; ++k) nd += !jobs[k].skip;
+    c->recs_off = at;
+    c->status_off = align16(at + nd * sizeof(NoiseAeadRecord));
+    c->payload_off = align16(c->status_off + nd);
+    size_t p = c->payload_off;
+    uint32_t desc = 0;
+    c->n_chacha = c->n_aes = 0;
+    /* ChaCha20-Poly1305 descriptors first, then AES-GCM: one ragged launch each */
     for (int pass = 0; pass < 2; ++pass) {
         int want = pass == 0 ? NOISE_CIPHER_CHACHAPOLY : NOISE_CIPHER_AESGCM;
-        for (size_t i = 0; i < n; ++i)
-            if (jobs[i].st->parent.cipher_id == want) order[slot++] = i;
-        if (pass == 0) n_chacha = slot;
+        for (size_t k = c->j0; k < c->j1; ++k) {
+            Job *j = &jobs[k];
+            if (j->skip || j->st->parent.cipher_id != want) continue;
+            j->desc = desc++;
+            j->ad_off = p;
+            p += align16(j->ad_len);
+            j->off = p;
+            p += slot_bytes(j->len);
+            if (pass == 0) ++c->n_chacha;
+            else ++c->n_aes;
+        }
     }
-    size_t p = payload_off;
-    for (size_t s = 0; s < n; ++s) {
-        Job *j = &jobs[order[s]];
-        NoiseAeadRecord *r = &recs[s];
-        r->ad_off = p;
-        r->ad_len = (uint32_t)j->ad_len;
-        if (j->ad_len) memcpy(sg->h + p, j->ad, j->ad_len);
-        p += align16(j->ad_len);
-        r->in_off = r->out_off = p;
-        memcpy(sg->h + p, j->data, j->len + (open ? 16 : 0));
-        p += slot_bytes(j->len);
-        r->len = (uint32_t)j->len;
+    c->end = p;
+    return (p + 63) & ~(size_t)63;
+}
+
+static void fill_descriptors(Job *jobs, const Chunk *c, uint8_t *h)
+{
+    NoiseAeadRecord *recs = (NoiseAeadRecord *)(h + c->recs_off);
+    for (size_t k = c->j0; k < c->j1; ++k) {
+        const Job *j = &jobs[k];
+        if (j->skip) continue;
+        NoiseAeadRecord *r = &recs[j->desc];
+        r->in_off = r->out_off = j->off;
         r->nonce = j->nonce;
         r->ctx_off = (uint64_t)(uintptr_t)j->st->d_ctx;
+        r->ad_off = j->ad_off;
+        r->len = (uint32_t)j->len;
+        r->ad_len = (uint32_t)j->ad_len;
     }
-    hipStream_t stream = sg->stream;
-    if (hipMemcpyAsync(sg->d, sg->h, p, hipMemcpyHostToDevice, stream) != hipSuccess)
-        rc = NOISE_ERROR_SYSTEM;
-    for (int c = 0; c < 2 && !rc; ++c) {
-        size_t first = c == 0 ? 0 : n_chacha, count = c == 0 ? n_chacha : n - n_chacha;
+}
+
+/* Chunk ci: H2D on the copy-in stream, then (on the main stream, after it)
+   the ragged kernels and the D2H of statuses + payload. */
+static int launch_chunk(Staging *sg, const Chunk *c, int ci, int open)
+{
+    if (hipMemcpyAsync(sg->d + c->recs_off, sg->h + c->recs_off, c->end - c->recs_off,
+                       hipMemcpyHostToDevice, sg->stream_in) != hipSuccess ||
+        hipEventRecord(sg->ev_in[ci], sg->stream_in) != hipSuccess ||
+        hipStreamWaitEvent(sg->stream, sg->ev_in[ci], 0) != hipSuccess)
+        return NOISE_ERROR_SYSTEM;
+    for (int k = 0; k < 2; ++k) {
+        uint32_t first = k == 0 ? 0 : c->n_chacha, count = k == 0 ? c->n_chacha : c->n_aes;
         if (!count) continue;
         NoiseAeadRagged job;
         job.ctx_base = NULL;
-        job.recs = (const NoiseAeadRecord *)(sg->d) + first;
+        job.recs = (const NoiseAeadRecord *)(sg->d + c->recs_off) + first;
         job.in = sg->d;
         job.out = sg->d;
         job.ad = sg->d;
-        job.status = sg->d + status_off + first;
-        job.n_records = (uint32_t)count;
+        job.status = sg->d + c->status_off + first;
+        job.n_records = count;
         job.lanes_per_record = 0;
         job.flags = NOISE_AEAD_FLAG_FAST;
         job.reserved_ = 0;
-        int cid = c == 0 ? NOISE_CIPHER_CHACHAPOLY : NOISE_CIPHER_AESGCM;
-        rc = open ? noise_aead_dev_open_ragged(cid, &job, stream)
-                  : noise_aead_dev_seal_ragged(cid, &job, stream);
+        int cid = k == 0 ? NOISE_CIPHER_CHACHAPOLY : NOISE_CIPHER_AESGCM;
+        int rc = open ? noise_aead_dev_open_ragged(cid, &job, sg->stream)
+                      : noise_aead_dev_seal_ragged(cid, &job, sg->stream);
+        if (rc) return rc;
     }
-    if (!rc && hipMemcpyAsync(sg->h + status_off, sg->d + status_off, p - status_off,
-                              hipMemcpyDeviceToHost, stream) != hipSuccess)
-        rc = NOISE_ERROR_SYSTEM;
-    if (!rc && hipStreamSynchronize(stream) != hipSuccess) rc = NOISE_ERROR_SYSTEM;
-    for (size_t s = 0; s < n; ++s) {
-        Job *j = &jobs[order[s]];
-        if (rc) {
-            j->status = NOISE_ERROR_SYSTEM;
-            continue;
-        }
-        const uint8_t *res = sg->h + recs[s].in_off;
-        j->result = NULL;
-        if (!open) {
-            memcpy(j->data, res, j->len + 16);
-            j->status = NOISE_ERROR_NONE;
-        } else if (sg->h[status_off + s] == 0) {
-            j->result = res;
-            j->status = NOISE_ERROR_NONE;
-        } else {
-            j->status = NOISE_ERROR_MAC_FAILURE;
+    if (hipMemcpyAsync(sg->h + c->status_off, sg->d + c->status_off, c->end - c->status_off,
+                       hipMemcpyDeviceToHost, sg->stream) != hipSuccess ||
+        hipEventRecord(sg->ev_out[ci], sg->stream) != hipSuccess)
+        return NOISE_ERROR_SYSTEM;
+    return NOISE_ERROR_NONE;
+}
+
+/* Wait for chunk ci, read its statuses, let `decide` pick the commits (seal:
+   every dispatched job), copy the results out and scrub staged plaintext. */
+static double now_ms(void);
+static int finish_chunk(Staging *sg, Job *jobs, const Chunk *c, int ci, int open,
+                        decide_fn decide, void *u, double *t_wait)
+{
+    double t0 = t_wait ? now_ms() : 0;
+    if (hipEventSynchronize(sg->ev_out[ci]) != hipSuccess) return NOISE_ERROR_SYSTEM;
+    if (t_wait) *t_wait += now_ms() - t0;
+    for (size_t k = c->j0; k < c->j1; ++k) {
+        Job *j = &jobs[k];
+        j->commit = j->defer = 0;
+        if (j->skip) continue;
+        j->status = !open || sg->h[c->status_off + j->desc] == 0 ? NOISE_ERROR_NONE
+                                                                 : NOISE_ERROR_MAC_FAILURE;
+        if (!decide) j->commit = j->status == NOISE_ERROR_NONE;
+    }
+    if (decide) decide(jobs, c->j0, c->j1, u);
+    CopyArg a = {jobs + c->j0, sg->h, open, c->payload_off};
+    host_pool_for(c->j1 - c->j0, copy_grain(c, c->j1 - c->j0), unpack_range, &a);
+    /* after seal the slots hold only CT || tag (the D2H overwrote every
+       staged plaintext byte); after open they hold verified plaintext */
+    if (open) host_pool_for(c->end - c->payload_off, (size_t)1 << 20, scrub_range, &a);
+    return NOISE_ERROR_NONE;
+}
+
+/* NOISE_AEAD_TRACE=1: one stderr line per pipelined call with the time the
+   calling thread spent packing, waiting for the GPU and unpacking. */
+static double now_ms(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+
+static int trace_on(void)
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("NOISE_AEAD_TRACE");
+        v = e && *e && *e != '0';
+    }
+    return v;
+}
+
+/* Run jobs (any mix of states and ciphers, record order) through the staging
+   pipeline.  Fills job.status for every dispatched job and applies the
+   commits `decide` selects (NULL: every verified job).  On a HIP error
+   returns NOISE_ERROR_SYSTEM; then no job of a chunk that was not finished
+   commits and their status is NOISE_ERROR_SYSTEM. */
+static int run_jobs(Job *jobs, size_t n, int open, decide_fn decide, void *u)
+{
+    if (n == 0) return NOISE_ERROR_NONE;
+    size_t total = 0;
+    for (size_t k = 0; k < n; ++k) {
+        jobs[k].status = jobs[k].skip ? NOISE_ERROR_INVALID_NONCE : NOISE_ERROR_SYSTEM;
+        jobs[k].commit = jobs[k].defer = 0;
+        total += job_bytes(&jobs[k]);
+    }
+    if (total == 0) { /* nothing to dispatch: only the decide step */
+        if (decide) decide(jobs, 0, n, u);
+        return NOISE_ERROR_NONE;
+    }
+    size_t target = total / (MAX_CHUNKS - 1) + 1;
+    if (target < CHUNK_MIN) target = CHUNK_MIN;
+    Chunk chunks[MAX_CHUNKS];
+    int nc = 0;
+    size_t at = 0, acc = 0, j0 = 0;
+    for (size_t k = 0; k < n; ++k) {
+        acc += job_bytes(&jobs[k]);
+        if (acc >= target || k + 1 == n) {
+            Chunk *c = &chunks[nc++];
+            c->j0 = j0;
+            c->j1 = k + 1;
+            at = plan_chunk(jobs, c, at);
+            j0 = k + 1;
+            acc = 0;
         }
     }
-    sg->scrub_off = payload_off;
-    sg->scrub_len = p - payload_off;
-    if (!open) stage_scrub();
-    free(order);
+    Staging *sg = stage_get(at + 64);
+    if (!sg) return NOISE_ERROR_SYSTEM;
+    int rc = NOISE_ERROR_NONE;
+    for (size_t k = 0; k < n && !rc; ++k)
+        if (!jobs[k].skip) rc = ensure_ctx(jobs[k].st, sg);
+
+    int launched = 0, finished = 0;
+    const int tr = trace_on();
+    double t_start = tr ? now_ms() : 0, t_pack = 0, t_fin = 0, t_wait = 0, t0 = 0;
+    for (int c = 0; c < nc && !rc; ++c) {
+        const Chunk *ch = &chunks[c];
+        if (tr) t0 = now_ms();
+        fill_descriptors(jobs, ch, sg->h);
+        CopyArg a = {jobs + ch->j0, sg->h, open, 0};
+        host_pool_for(ch->j1 - ch->j0, copy_grain(ch, ch->j1 - ch->j0), pack_range, &a);
+        if (tr) t_pack += now_ms() - t0;
+        rc = launch_chunk(sg, ch, c, open);
+        if (rc) break;
+        ++launched;
+        if (c > 0) {
+            if (tr) t0 = now_ms();
+            rc = finish_chunk(sg, jobs, &chunks[c - 1], c - 1, open, decide, u, tr ? &t_wait : NULL);
+            if (tr) t_fin += now_ms() - t0;
+            if (rc) break;
+            ++finished;
+        }
+    }
+    if (!rc && finished < launched) {
+        if (tr) t0 = now_ms();
+        rc = finish_chunk(sg, jobs, &chunks[launched - 1], launched - 1, open, decide, u, tr ? &t_wait : NULL);
+        if (tr) t_fin += now_ms() - t0;
+        if (!rc) ++finished;
+    }
+    if (tr)
+        fprintf(stderr, "noise_aead %s: %zu jobs, %d chunks, %zu B staged, %d threads: "
+                "total %.3f ms, pack %.3f, finish %.3f (of which GPU wait %.3f)\n",
+                open ? "open" : "seal", n, nc, at, host_pool_threads(), now_ms() - t_start,
+                t_pack, t_fin, t_wait);
+    if (rc) { /* drain, fail what did not finish, leave no plaintext behind */
+        (void)hipStreamSynchronize(sg->stream_in);
+        (void)hipStreamSynchronize(sg->stream);
+        for (int c = finished; c < nc; ++c)
+            for (size_t k = chunks[c].j0; k < chunks[c].j1; ++k) {
+                jobs[k].status = NOISE_ERROR_SYSTEM;
+                jobs[k].commit = jobs[k].defer = 0;
+            }
+        size_t from = finished < nc ? chunks[finished].recs_off : at;
+        if (at > from) explicit_bzero(sg->h + from, at - from);
+    }
     return rc;
 }
 
@@ -335,10 +511,9 @@ static int hip_crypt(NoiseCipherState *state, const uint8_t *ad, size_t ad_len,
     j.data = data;
     j.len = len;
     j.nonce = state->n; /* the backend reads n; the front end owns n++ */
-    j.status = NOISE_ERROR_SYSTEM;
-    int rc = run_jobs(&j, 1, open);
-    if (!rc && open && j.status == NOISE_ERROR_NONE) memcpy(data, j.result, len);
-    stage_scrub();
+    j.idx = 0;
+    j.skip = 0;
+    int rc = run_jobs(&j, 1, open, NULL, NULL);
     return rc ? rc : j.status;
 }
 
@@ -551,12 +726,7 @@ int noise_cipherstate_encrypt_batch(NoiseCipherState *const *states, const uint8
 {
     if ((!states || !buffers || !results) && count) return NOISE_ERROR_INVALID_PARAM;
     Job *jobs = (Job *)malloc((count ? count : 1) * sizeof(Job));
-    size_t *idx = (size_t *)malloc((count ? count : 1) * sizeof(size_t));
-    if (!jobs || !idx) {
-        free(jobs);
-        free(idx);
-        return NOISE_ERROR_NO_MEMORY;
-    }
+    if (!jobs) return NOISE_ERROR_NO_MEMORY;
     size_t nj = 0;
     for (size_t i = 0; i < count; ++i) {
         NoiseCipherState *st = states[i];
@@ -569,24 +739,59 @@ int noise_cipherstate_encrypt_batch(NoiseCipherState *const *states, const uint8
         int pass;
         results[i] = check_encrypt(st, ad, ad_len, &buffers[i], &pass);
         if (results[i] || pass) continue;
-        Job *j = &jobs[nj];
+        Job *j = &jobs[nj++];
         j->st = (HipCipherState *)st;
         j->ad = ad;
         j->ad_len = ad_len;
         j->data = buffers[i].data;
         j->len = buffers[i].size;
-        j->nonce = st->n++;
-        idx[nj++] = i;
+        j->nonce = st->n++; /* advanced even if the backend fails (cipherstate.c:325-326) */
+        j->idx = i;
+        j->skip = 0;
     }
-    int rc = run_jobs(jobs, nj, 0);
+    int rc = run_jobs(jobs, nj, 0, NULL, NULL);
     for (size_t k = 0; k < nj; ++k) {
-        size_t i = idx[k];
+        size_t i = jobs[k].idx;
         results[i] = jobs[k].status;
         if (jobs[k].status == NOISE_ERROR_NONE) buffers[i].size += 16;
     }
     free(jobs);
-    free(idx);
     return rc;
+}
+
+typedef struct {
+    NoiseBuffer *buffers;
+    int *results;
+} OpenBatch;
+
+/* The sequential semantics of noise_cipherstate_decrypt_with_ad
+   (cipherstate.c:373-410) applied in record order: a MAC failure leaves the
+   record and n untouched, and every later record of that state depends on n,
+   so it is deferred to the next round instead of committed. */
+static void open_batch_decide(Job *jobs, size_t lo, size_t hi, void *u)
+{
+    OpenBatch *b = (OpenBatch *)u;
+    for (size_t k = lo; k < hi; ++k) {
+        Job *j = &jobs[k];
+        HipCipherState *st = j->st;
+        j->commit = j->defer = 0;
+        if (st->b_failed) {
+            j->defer = 1;
+            continue;
+        }
+        if (j->skip) { /* nonce exhausted (cipherstate.c:391-397) */
+            b->results[j->idx] = NOISE_ERROR_INVALID_NONCE;
+            continue;
+        }
+        b->results[j->idx] = j->status;
+        if (j->status == NOISE_ERROR_NONE) {
+            j->commit = 1;
+            ++st->parent.n;
+            b->buffers[j->idx].size -= 16;
+        } else {
+            st->b_failed = 1;
+        }
+    }
 }
 
 int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8_t *const *ads,
@@ -597,11 +802,9 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
     static uint64_t epoch_counter = 0;
     Job *jobs = (Job *)malloc((count ? count : 1) * sizeof(Job));
     size_t *pend = (size_t *)malloc((count ? count : 1) * sizeof(size_t));
-    size_t *idx = (size_t *)malloc((count ? count : 1) * sizeof(size_t));
-    if (!jobs || !pend || !idx) {
+    if (!jobs || !pend) {
         free(jobs);
         free(pend);
-        free(idx);
         return NOISE_ERROR_NO_MEMORY;
     }
     /* Round 1 validates everything; records whose outcome depends on an
@@ -621,10 +824,10 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
         if (results[i] || pass) continue;
         pend[np++] = i;
     }
+    OpenBatch ob = {buffers, results};
     int rc = NOISE_ERROR_NONE;
     while (np && !rc) {
         const uint64_t epoch = __atomic_add_fetch(&epoch_counter, 1, __ATOMIC_RELAXED);
-        size_t nj = 0, nnext = 0;
         for (size_t p = 0; p < np; ++p) {
             size_t i = pend[p];
             HipCipherState *st = (HipCipherState *)states[i];
@@ -633,56 +836,30 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
                 st->b_next = st->parent.n;
                 st->b_failed = 0;
             }
-            Job *j = &jobs[nj];
+            Job *j = &jobs[p];
             j->st = st;
             j->ad = ads ? ads[i] : NULL;
             j->ad_len = ad_lens ? ad_lens[i] : 0;
             j->data = buffers[i].data;
             j->len = buffers[i].size - 16;
+            j->idx = i;
             /* assumes the earlier records of the state verify; an exhausted
                nonce stays exhausted (cipherstate.c:391-397) */
             j->nonce = st->b_next;
-            if (st->b_next != NONCE_LIMIT) ++st->b_next;
-            idx[nj++] = i;
+            j->skip = st->b_next == NONCE_LIMIT;
+            if (!j->skip) ++st->b_next;
         }
-        /* nonce exhaustion is checked before dispatch */
-        size_t keep = 0;
-        for (size_t k = 0; k < nj; ++k) {
-            if (jobs[k].nonce == NONCE_LIMIT) continue;
-            jobs[keep] = jobs[k];
-            idx[keep++] = idx[k];
-        }
-        rc = run_jobs(jobs, keep, 1);
-        /* apply in record order */
-        size_t k = 0;
+        rc = run_jobs(jobs, np, 1, open_batch_decide, &ob);
+        size_t nnext = 0;
         for (size_t p = 0; p < np; ++p) {
-            size_t i = pend[p];
-            HipCipherState *st = (HipCipherState *)states[i];
-            int dispatched = (k < keep && idx[k] == i);
-            if (st->b_failed) { /* depends on a failure earlier in this round */
-                pend[nnext++] = i;
-                if (dispatched) ++k;
-                continue;
-            }
-            if (!dispatched) { /* nonce exhausted */
-                results[i] = NOISE_ERROR_INVALID_NONCE;
-                continue;
-            }
-            Job *j = &jobs[k++];
-            results[i] = j->status;
-            if (j->status == NOISE_ERROR_NONE) {
-                memcpy(j->data, j->result, j->len);
-                ++st->parent.n;
-                buffers[i].size -= 16;
-            } else {
-                st->b_failed = 1;
-            }
+            if (rc) {
+                if (jobs[p].defer || jobs[p].status == NOISE_ERROR_SYSTEM)
+                    results[jobs[p].idx] = NOISE_ERROR_SYSTEM;
+            } else if (jobs[p].defer) pend[nnext++] = jobs[p].idx;
         }
-        stage_scrub();
         np = nnext;
     }
     free(jobs);
     free(pend);
-    free(idx);
     return rc;
 }
