@@ -121,6 +121,46 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states,
                                     const uint8_t *const *ads, const size_t *ad_lens,
                                     NoiseBuffer *buffers, size_t count, int *results);
 
+/* ------------------------------------------------ 3b. transport wire buffers
+ *
+ * SURVEY.md §8f rank 1.  A wire buffer holds frames in the format of the
+ * reference's examples/echo (echo-common.c:643-688, echo_recv/echo_send):
+ * a 2-byte big-endian length L, then L bytes of CT || tag.  These calls work
+ * in place on every complete frame at the start of the buffer, frame k under
+ * nonce n + k of its CipherState, in one pipelined GPU pass:
+ *
+ *   noise_wire_seal : each frame holds L - 16 bytes of plaintext followed by
+ *                     16 bytes of room; they become CT || tag.  The header is
+ *                     already the final length (what echo_send writes).
+ *   noise_wire_open : each frame's first L - 16 bytes become its plaintext
+ *                     (the 16 tag bytes after it are left as they were).
+ *   noise_wire_echo : the echo server's transport loop (echo-server.c
+ *                     :377-407): every frame opened with `recv` and sealed
+ *                     again with `send` (same length, so in place).
+ *
+ * *frames / *consumed report the frames processed and the bytes they span.
+ * Processing stops, exactly as the per-frame CipherState calls would, at:
+ *   - a partial frame at the end (returns NOISE_ERROR_NONE);
+ *   - a frame with L < 16 (NOISE_ERROR_INVALID_LENGTH) or an exhausted
+ *     nonce (NOISE_ERROR_INVALID_NONCE) — that frame is untouched;
+ *   - open/echo: the first frame whose tag fails (NOISE_ERROR_MAC_FAILURE):
+ *     it and every later frame are untouched and n stays at its nonce, the
+ *     rule of cipherstate.c:400-405 applied frame by frame.
+ * Nonces advance by the frames processed (seal: by every frame dispatched,
+ * also on NOISE_ERROR_SYSTEM, as cipherstate.c:325-326).  The states must be
+ * keyed (NOISE_ERROR_INVALID_STATE otherwise) and, for echo, distinct.
+ *
+ * Buffers from noise_wire_alloc() are pinned host memory: H2D and D2H use
+ * them directly.  Any other buffer is staged through pinned memory. */
+void *noise_wire_alloc(size_t bytes);
+void noise_wire_free(void *wire);
+int noise_wire_seal(NoiseCipherState *state, uint8_t *wire, size_t wire_len,
+                    size_t *consumed, size_t *frames);
+int noise_wire_open(NoiseCipherState *state, uint8_t *wire, size_t wire_len,
+                    size_t *consumed, size_t *frames);
+int noise_wire_echo(NoiseCipherState *recv, NoiseCipherState *send, uint8_t *wire,
+                    size_t wire_len, size_t *consumed, size_t *frames);
+
 /* ------------------------------------------------ 4. device-resident API
  *
  * All pointers below are device pointers on the current HIP device; `stream`

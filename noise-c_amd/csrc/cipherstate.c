@@ -10,7 +10,7 @@
  * bytes and launches.
  */
 #define _DEFAULT_SOURCE
-#include "noise_aead_hip.h"
+#include "host_internal.h"
 #include "host_pool.h"
 
 #include <hip/hip_runtime_api.h>
@@ -20,46 +20,9 @@
 #include <stdio.h>
 #include <time.h>
 
-/* ------------------------------------------------- the plugin object ABI */
-
-/* Identical layout to struct NoiseCipherState_s, src/protocol/internal.h:58-146. */
-struct NoiseCipherState_s {
-    size_t size;
-    int cipher_id;
-    uint8_t has_key;
-    uint8_t key_len;
-    uint8_t mac_len;
-    uint64_t n;
-    NoiseCipherState *(*create)(void);
-    void (*init_key)(NoiseCipherState *state, const uint8_t *key);
-    int (*encrypt)(NoiseCipherState *state, const uint8_t *ad, size_t ad_len,
-                   uint8_t *data, size_t len);
-    int (*decrypt)(NoiseCipherState *state, const uint8_t *ad, size_t ad_len,
-                   uint8_t *data, size_t len);
-    void (*destroy)(NoiseCipherState *state);
-};
-
-#define MAX_KEY_LEN 32 /* cipherstate.c:53 */
-#define MAX_MAC_LEN 16 /* cipherstate.c:56 */
-#define NONCE_LIMIT 0xFFFFFFFFFFFFFFFFULL
-
-/* Backend state appended by first-member embedding, as cipher-chachapoly.c
-   :28-35 and cipher-aesgcm.c:28-36 do. */
-typedef struct {
-    struct NoiseCipherState_s parent;
-    uint8_t key[32];
-    void *d_ctx;       /* device key context (noise_aead_dev_ctx_bytes) */
-    int device;        /* HIP device that owns d_ctx */
-    int ctx_ready;     /* d_ctx matches key */
-    /* scratch for the batch walker (a CipherState is single-owner) */
-    uint64_t b_epoch;
-    uint64_t b_next;   /* nonce the next record of this batch round will use */
-    int b_failed;
-} HipCipherState;
-
 /* ---------------------------------------------------- util.c equivalents */
 
-static void clean(void *p, size_t n) /* util.c:170-177 noise_clean */
+void na_clean(void *p, size_t n) /* util.c:170-177 noise_clean */
 {
     volatile uint8_t *d = (volatile uint8_t *)p;
     while (n--) *d++ = 0;
@@ -75,7 +38,7 @@ static void *new_object(size_t size) /* util.c:135-142 noise_new_object */
 static void free_object(void *ptr, size_t size) /* util.c:152-158 noise_free */
 {
     if (!ptr) return;
-    clean(ptr, size);
+    na_clean(ptr, size);
     free(ptr);
 }
 
@@ -86,19 +49,6 @@ static void free_object(void *ptr, size_t size) /* util.c:152-158 noise_free */
      host threads pack chunk c+1 while chunk c crosses PCIe (copy-in stream)
      and runs on the GPU, and the host unpacks chunk c-1 as its D2H lands.
    H2D and D2H use different streams, so both PCIe directions are busy. */
-#define MAX_CHUNKS 64
-#define CHUNK_MIN ((size_t)4 << 20)
-
-typedef struct {
-    int device;
-    hipStream_t stream;    /* kernels + D2H */
-    hipStream_t stream_in; /* H2D */
-    hipEvent_t ev_in[MAX_CHUNKS], ev_out[MAX_CHUNKS];
-    uint8_t *h;        /* pinned host */
-    uint8_t *d;        /* device */
-    size_t cap;
-} Staging;
-
 static pthread_key_t g_stage_key;
 static pthread_once_t g_stage_once = PTHREAD_ONCE_INIT;
 
@@ -111,7 +61,9 @@ static void stage_destroy(void *p)
     for (int i = 0; i < MAX_CHUNKS; ++i) {
         if (s->ev_in[i]) (void)hipEventDestroy(s->ev_in[i]);
         if (s->ev_out[i]) (void)hipEventDestroy(s->ev_out[i]);
+        if (s->ev_done[i]) (void)hipEventDestroy(s->ev_done[i]);
     }
+    if (s->stream_out) (void)hipStreamDestroy(s->stream_out);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     if (s->stream_in) (void)hipStreamDestroy(s->stream_in);
     free(s);
@@ -120,7 +72,7 @@ static void stage_destroy(void *p)
 static void stage_key_init(void) { pthread_key_create(&g_stage_key, stage_destroy); }
 
 /* Staging area of at least `bytes` on the current device, or NULL. */
-static Staging *stage_get(size_t bytes)
+Staging *na_stage_get(size_t bytes)
 {
     pthread_once(&g_stage_once, stage_key_init);
     int dev = 0;
@@ -136,10 +88,12 @@ static Staging *stage_get(size_t bytes)
         if (!s) return NULL;
         s->device = dev;
         int ok = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) == hipSuccess &&
-                 hipStreamCreateWithFlags(&s->stream_in, hipStreamNonBlocking) == hipSuccess;
+                 hipStreamCreateWithFlags(&s->stream_in, hipStreamNonBlocking) == hipSuccess &&
+                 hipStreamCreateWithFlags(&s->stream_out, hipStreamNonBlocking) == hipSuccess;
         for (int i = 0; ok && i < MAX_CHUNKS; ++i)
             ok = hipEventCreateWithFlags(&s->ev_in[i], hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&s->ev_out[i], hipEventDisableTiming) == hipSuccess;
+                 hipEventCreateWithFlags(&s->ev_out[i], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&s->ev_done[i], hipEventDisableTiming) == hipSuccess;
         if (!ok) {
             stage_destroy(s);
             return NULL;
@@ -163,11 +117,10 @@ static Staging *stage_get(size_t bytes)
 
 /* --------------------------------------------------- device key contexts */
 
-static int is_ours(const NoiseCipherState *st);
 
 /* Build the device key context of `st` from its key (lazy: init_key has no
    error return in the plugin ABI, internal.h:95). */
-static int ensure_ctx(HipCipherState *st, Staging *sg)
+int na_ensure_ctx(HipCipherState *st, Staging *sg)
 {
     if (st->ctx_ready) return NOISE_ERROR_NONE;
     int dev = sg->device;
@@ -192,7 +145,7 @@ static int ensure_ctx(HipCipherState *st, Staging *sg)
     int rc = noise_aead_dev_prepare(st->parent.cipher_id, d, 1, st->d_ctx, sg->stream);
     if (rc) return rc;
     if (hipStreamSynchronize(sg->stream) != hipSuccess) return NOISE_ERROR_SYSTEM;
-    clean(h, 32);
+    na_clean(h, 32);
     st->ctx_ready = 1;
     return NOISE_ERROR_NONE;
 }
@@ -363,13 +316,12 @@ static int launch_chunk(Staging *sg, const Chunk *c, int ci, int open)
 
 /* Wait for chunk ci, read its statuses, let `decide` pick the commits (seal:
    every dispatched job), copy the results out and scrub staged plaintext. */
-static double now_ms(void);
 static int finish_chunk(Staging *sg, Job *jobs, const Chunk *c, int ci, int open,
                         decide_fn decide, void *u, double *t_wait)
 {
-    double t0 = t_wait ? now_ms() : 0;
+    double t0 = t_wait ? na_now_ms() : 0;
     if (hipEventSynchronize(sg->ev_out[ci]) != hipSuccess) return NOISE_ERROR_SYSTEM;
-    if (t_wait) *t_wait += now_ms() - t0;
+    if (t_wait) *t_wait += na_now_ms() - t0;
     for (size_t k = c->j0; k < c->j1; ++k) {
         Job *j = &jobs[k];
         j->commit = j->defer = 0;
@@ -389,14 +341,14 @@ static int finish_chunk(Staging *sg, Job *jobs, const Chunk *c, int ci, int open
 
 /* NOISE_AEAD_TRACE=1: one stderr line per pipelined call with the time the
    calling thread spent packing, waiting for the GPU and unpacking. */
-static double now_ms(void)
+double na_now_ms(void)
 {
     struct timespec t;
     clock_gettime(CLOCK_MONOTONIC, &t);
     return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
 }
 
-static int trace_on(void)
+int na_trace_on(void)
 {
     static int v = -1;
     if (v < 0) {
@@ -440,43 +392,43 @@ static int run_jobs(Job *jobs, size_t n, int open, decide_fn decide, void *u)
             acc = 0;
         }
     }
-    Staging *sg = stage_get(at + 64);
+    Staging *sg = na_stage_get(at + 64);
     if (!sg) return NOISE_ERROR_SYSTEM;
     int rc = NOISE_ERROR_NONE;
     for (size_t k = 0; k < n && !rc; ++k)
-        if (!jobs[k].skip) rc = ensure_ctx(jobs[k].st, sg);
+        if (!jobs[k].skip) rc = na_ensure_ctx(jobs[k].st, sg);
 
     int launched = 0, finished = 0;
-    const int tr = trace_on();
-    double t_start = tr ? now_ms() : 0, t_pack = 0, t_fin = 0, t_wait = 0, t0 = 0;
+    const int tr = na_trace_on();
+    double t_start = tr ? na_now_ms() : 0, t_pack = 0, t_fin = 0, t_wait = 0, t0 = 0;
     for (int c = 0; c < nc && !rc; ++c) {
         const Chunk *ch = &chunks[c];
-        if (tr) t0 = now_ms();
+        if (tr) t0 = na_now_ms();
         fill_descriptors(jobs, ch, sg->h);
         CopyArg a = {jobs + ch->j0, sg->h, open, 0};
         host_pool_for(ch->j1 - ch->j0, copy_grain(ch, ch->j1 - ch->j0), pack_range, &a);
-        if (tr) t_pack += now_ms() - t0;
+        if (tr) t_pack += na_now_ms() - t0;
         rc = launch_chunk(sg, ch, c, open);
         if (rc) break;
         ++launched;
         if (c > 0) {
-            if (tr) t0 = now_ms();
+            if (tr) t0 = na_now_ms();
             rc = finish_chunk(sg, jobs, &chunks[c - 1], c - 1, open, decide, u, tr ? &t_wait : NULL);
-            if (tr) t_fin += now_ms() - t0;
+            if (tr) t_fin += na_now_ms() - t0;
             if (rc) break;
             ++finished;
         }
     }
     if (!rc && finished < launched) {
-        if (tr) t0 = now_ms();
+        if (tr) t0 = na_now_ms();
         rc = finish_chunk(sg, jobs, &chunks[launched - 1], launched - 1, open, decide, u, tr ? &t_wait : NULL);
-        if (tr) t_fin += now_ms() - t0;
+        if (tr) t_fin += na_now_ms() - t0;
         if (!rc) ++finished;
     }
     if (tr)
         fprintf(stderr, "noise_aead %s: %zu jobs, %d chunks, %zu B staged, %d threads: "
                 "total %.3f ms, pack %.3f, finish %.3f (of which GPU wait %.3f)\n",
-                open ? "open" : "seal", n, nc, at, host_pool_threads(), now_ms() - t_start,
+                open ? "open" : "seal", n, nc, at, host_pool_threads(), na_now_ms() - t_start,
                 t_pack, t_fin, t_wait);
     if (rc) { /* drain, fail what did not finish, leave no plaintext behind */
         (void)hipStreamSynchronize(sg->stream_in);
@@ -569,7 +521,7 @@ NoiseCipherState *noise_aesgcm_new(void)
     return hip_new(NOISE_CIPHER_AESGCM, noise_aesgcm_new);
 }
 
-static int is_ours(const NoiseCipherState *st) { return st && st->encrypt == hip_encrypt; }
+int na_is_ours(const NoiseCipherState *st) { return st && st->encrypt == hip_encrypt; }
 
 /* ------------------------------------------ CipherState API (cipherstate.c) */
 
@@ -732,7 +684,7 @@ int noise_cipherstate_encrypt_batch(NoiseCipherState *const *states, const uint8
         NoiseCipherState *st = states[i];
         const uint8_t *ad = ads ? ads[i] : NULL;
         size_t ad_len = ad_lens ? ad_lens[i] : 0;
-        if (st && !is_ours(st)) { /* a foreign plugin object: its own backend */
+        if (st && !na_is_ours(st)) { /* a foreign plugin object: its own backend */
             results[i] = noise_cipherstate_encrypt_with_ad(st, ad, ad_len, &buffers[i]);
             continue;
         }
@@ -815,7 +767,7 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
         NoiseCipherState *st = states[i];
         const uint8_t *ad = ads ? ads[i] : NULL;
         size_t ad_len = ad_lens ? ad_lens[i] : 0;
-        if (st && !is_ours(st)) {
+        if (st && !na_is_ours(st)) {
             results[i] = noise_cipherstate_decrypt_with_ad(st, ad, ad_len, &buffers[i]);
             continue;
         }

@@ -5,10 +5,14 @@
  */
 #define _GNU_SOURCE
 #include "host_pool.h"
+#include "host_internal.h"
 
 #include <pthread.h>
 #include <sched.h>
 #include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
+#include <emmintrin.h>
 
 #define MAX_THREADS 64
 
@@ -124,4 +128,30 @@ void host_pool_for(size_t n, size_t grain, pool_fn fn, void *arg)
     while (P.active) pthread_cond_wait(&P.done, &P.mu);
     pthread_mutex_unlock(&P.mu);
     pthread_mutex_unlock(&P.busy);
+}
+
+__attribute__((visibility("hidden"))) void na_copy_stream(uint8_t *dst, const uint8_t *src,
+                                                          size_t n)
+{
+    if (n < 256) {
+        memcpy(dst, src, n);
+        return;
+    }
+    size_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+    memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    for (; n >= 64; n -= 64, dst += 64, src += 64) {
+        __m128i x0 = _mm_loadu_si128((const __m128i *)src);
+        __m128i x1 = _mm_loadu_si128((const __m128i *)(src + 16));
+        __m128i x2 = _mm_loadu_si128((const __m128i *)(src + 32));
+        __m128i x3 = _mm_loadu_si128((const __m128i *)(src + 48));
+        _mm_stream_si128((__m128i *)dst, x0);
+        _mm_stream_si128((__m128i *)(dst + 16), x1);
+        _mm_stream_si128((__m128i *)(dst + 32), x2);
+        _mm_stream_si128((__m128i *)(dst + 48), x3);
+    }
+    memcpy(dst, src, n);
+    _mm_sfence();
 }

@@ -21,11 +21,11 @@ extern "C" {
    inline when the pool has one thread, is busy with another caller, or n is
    at most one grain. */
 typedef void (*pool_fn)(void *arg, size_t lo, size_t hi);
-void host_pool_for(size_t n, size_t grain, pool_fn fn, void *arg);
+__attribute__((visibility("hidden"))) void host_pool_for(size_t n, size_t grain, pool_fn fn, void *arg);
 
 /* Threads the pool uses (NOISE_AEAD_HOST_THREADS, else min(16, CPUs this
    process may run on)). */
-int host_pool_threads(void);
+__attribute__((visibility("hidden"))) int host_pool_threads(void);
 
 #ifdef __cplusplus
 }

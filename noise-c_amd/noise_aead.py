@@ -118,6 +118,11 @@ def lib() -> C.CDLL:
         "noise_aesgcm_new": (vp, []),
         "noise_cipherstate_encrypt_batch": (i, [P(vp), P(vp), P(sz), P(NoiseBuffer), sz, P(i)]),
         "noise_cipherstate_decrypt_batch": (i, [P(vp), P(vp), P(sz), P(NoiseBuffer), sz, P(i)]),
+        "noise_wire_alloc": (vp, [sz]),
+        "noise_wire_free": (None, [vp]),
+        "noise_wire_seal": (i, [vp, vp, sz, P(sz), P(sz)]),
+        "noise_wire_open": (i, [vp, vp, sz, P(sz), P(sz)]),
+        "noise_wire_echo": (i, [vp, vp, vp, sz, P(sz), P(sz)]),
         "noise_aead_dev_ctx_bytes": (sz, [i]),
         "noise_aead_dev_prepare": (i, [i, vp, C.c_uint32, vp, vp]),
         "noise_aead_dev_seal_uniform": (i, [i, P(NoiseAeadUniform), vp]),
@@ -133,6 +138,68 @@ def lib() -> C.CDLL:
         f.argtypes = args
     _LIB = L
     return L
+
+
+# ---------------------------------------------------------------- wire path
+# Frames of examples/echo (echo-common.c:643-688): 2-byte BE length || body.
+
+def frame_for_seal(messages) -> bytes:
+    """Seal-ready wire image: each message as one frame whose header is the
+    final length (len + 16) followed by the plaintext and 16 bytes of room."""
+    out = bytearray()
+    for m in messages:
+        L = len(m) + 16
+        if L > MAX_PAYLOAD_LEN:
+            raise ValueError("message too long for one frame")
+        out += bytes((L >> 8, L & 0xFF)) + bytes(m) + bytes(16)
+    return bytes(out)
+
+
+def parse_frames(wire: bytes, count=None):
+    """[(offset of the body, L)] of the complete frames at the start of wire."""
+    out, off = [], 0
+    while off + 2 <= len(wire) and (count is None or len(out) < count):
+        L = (wire[off] << 8) | wire[off + 1]
+        if off + 2 + L > len(wire):
+            break
+        out.append((off + 2, L))
+        off += 2 + L
+    return out
+
+
+def _wire_call(fn, states, buf, length):
+    consumed, frames = C.c_size_t(), C.c_size_t()
+    rc = fn(*[s.ptr for s in states], buf, length, C.byref(consumed), C.byref(frames))
+    return rc, consumed.value, frames.value
+
+
+def wire_seal(state, buf, length):
+    """noise_wire_seal over a ctypes buffer / address; (rc, consumed, frames)."""
+    return _wire_call(lib().noise_wire_seal, [state], buf, length)
+
+
+def wire_open(state, buf, length):
+    return _wire_call(lib().noise_wire_open, [state], buf, length)
+
+
+def wire_echo(recv, send, buf, length):
+    return _wire_call(lib().noise_wire_echo, [recv, send], buf, length)
+
+
+class PinnedWire:
+    """A noise_wire_alloc() buffer (pinned host memory), freed on close()."""
+
+    def __init__(self, nbytes: int):
+        self.n = nbytes
+        self.addr = lib().noise_wire_alloc(nbytes)
+        if not self.addr:
+            raise MemoryError("noise_wire_alloc failed")
+        self.view = (C.c_uint8 * nbytes).from_address(self.addr)
+
+    def close(self):
+        if self.addr:
+            lib().noise_wire_free(self.addr)
+            self.addr = None
 
 
 def _bytes_ptr(b):
@@ -188,6 +255,12 @@ class CipherState:
         k = _bytes_ptr(key) if key is not None else None
         return lib().noise_cipherstate_init_key(
             self.ptr, k, len(key) if key_len is None else key_len)
+
+    @property
+    def nonce(self) -> int:
+        """n of the state: the u64 at offset 16 of struct NoiseCipherState_s
+        (internal.h:58-146; there is no getter in the reference API)."""
+        return C.c_uint64.from_address(self.ptr.value + 16).value
 
     def set_nonce(self, n: int) -> int:
         return lib().noise_cipherstate_set_nonce(self.ptr, n)
