@@ -207,3 +207,17 @@ def test_wire_stops_at_short_frame_and_exhausted_nonce(aead, gpu, oracle):
     assert (rc, frames) == (A.ERROR_INVALID_NONCE, 3) and st.nonce == NONCE_MAX
     assert bytes(b)[:consumed] == _sealed_wire(oracle, CHACHA, key, NONCE_MAX - 3, msgs[:3])
     st.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cipher", ["chachapoly", "aesgcm"])
+def test_echo_loopback_tcp(aead, gpu, cipher):
+    """Config C1's plumbing over a real 127.0.0.1 socket: bursts whose bytes
+    reach the server in arbitrary recv() pieces (partial frames carried over),
+    every echo decrypted by the client and compared with what it sent."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools"))
+    import echo_loopback
+    r = echo_loopback.run(messages=3000, size=1024, burst=700, cipher=cipher)
+    assert r["verified"] and r["server_error"] == 0
+    assert r["server_frames"] == 3000
