@@ -43,6 +43,10 @@ CONFIGS = {
                workload="AES-256-GCM 64Ki x 1400B records, one CipherState key"),
     "c4": dict(cipher=CHACHA, records=1048576, len=1400, states=4096,
                workload="ChaCha20-Poly1305 1Mi x 1400B records, 4096 CipherStates x 256"),
+    # noise-c's own tests/performance perf_cipher shape (test-performance.c
+    # :140-179): 1024-B records with 32 B of associated data each
+    "perf": dict(cipher=CHACHA, records=65536, len=1024, states=1, ad=32,
+                 workload="ChaCha20-Poly1305 64Ki x 1024B records + 32B AD (tests/performance shape)"),
     # C5 per GPU = 1/8 of the 8-GPU job (1 Mi records, 4096 states in total):
     # lengths 64 + splitmix64(seed_len + i) mod 16321, cipher by state parity.
     "c5": dict(cipher=None, records=131072, len=None, states=512,
@@ -115,6 +119,13 @@ def cpu_baseline(cfg, budget_cpu_s: float = 12.0):
     if not os.path.exists(ref):
         return None
     cname = "aesgcm" if cfg["cipher"] == AES else "chachapoly"
+    if cfg.get("ad"):  # the reference's own perf_cipher loop, unchanged: 1 thread, encrypt only
+        out = subprocess.run([ref, "perf", cname, str(cfg["len"]), "200000", "1"],
+                             capture_output=True, text=True, timeout=300, check=True)
+        r = json.loads(out.stdout)
+        return {"value": round(r["mib_per_s"] / 1024.0, 4), "unit": "GiB/s", "cores": 1,
+                "kind": kind, "sample": f"tests/performance perf_cipher {cname}: 200000 x "
+                f"1024 B + 32 B AD encrypts, one thread, CPU-time clock (encrypt only)"}
     try:
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -153,14 +164,33 @@ def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length):
     return f"chachapoly_seal_uniform<{lanes}, {'true' if fast else 'false'}>"
 
 
-def load_traffic(config_name: str, kernel: str):
+def load_pmc(config_name: str, kernel: str):
+    """Per-launch PMC counters of `kernel` from profiles/traffic_<cfg>.json
+    (tools/gpu/pmc.sh + tools/pmc_report.py), or {}."""
     path = os.path.join(ROOT, "profiles", f"traffic_{config_name}.json")
     if not os.path.exists(path):
-        return None
+        return {}
     with open(path) as f:
         t = json.load(f)
-    k = t.get("kernels", {}).get(kernel)
-    return None if k is None else k.get("hbm_bytes_per_launch")
+    return t.get("kernels", {}).get(kernel) or {}
+
+
+# VALU issue ceiling (DESIGN.md §5): a SIMD issues one wave64 integer VALU
+# instruction per ~4 cycles for the shift/rotate/multiply class and whenever
+# fast (add/xor) and slow ops interleave (profiles/r01_rates_dep.log), so the
+# chip-wide ceiling is 1024 SIMDs x 2.4 GHz / 4 wave-instructions per second.
+VALU_ISSUE_PEAK = 1024 * 2.4e9 / 4
+
+
+def issue_bound(pmc, avg_launch_ms):
+    n = pmc.get("SQ_INSTS_VALU")
+    if not n or not avg_launch_ms:
+        return None
+    rate = n / (avg_launch_ms * 1e-3)
+    return {"resource": "VALU issue (wave-instructions/s)", "valu_insts_per_launch": int(n),
+            "achieved": round(rate / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
+            "unit": "G wave-instr/s", "frac": round(rate / VALU_ISSUE_PEAK, 4),
+            "source": "SQ_INSTS_VALU from the committed PMC profile / live launch time"}
 
 
 def main():
@@ -210,6 +240,12 @@ def main():
     assert A.dev_prepare(cipher, raw.data_ptr(), len(sh["key_ids"]), ctx.data_ptr(), sp) == 0
     nonce = torch.tensor(sh["nonce_base"], dtype=torch.int64, device=dev)
     del key_ids
+    AD = cfg.get("ad", 0)
+    ad_buf = None
+    if AD:
+        ad_buf = torch.empty(N * AD, dtype=torch.uint8, device=dev)
+        assert A.dev_fill_splitmix(ad_buf.data_ptr(), ad_buf.numel(), 0x6164, sh["first"] * AD // 8, sp) == 0
+    ad_kw = dict(ad=ad_buf.data_ptr() if AD else 0, ad_stride=AD, ad_len=AD)
 
     sets = []
     for b in range(args.sets):
@@ -231,7 +267,7 @@ def main():
         return A.dev_uniform(False, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
                              inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
                              out_stride=out_stride, length=L, n_records=N,
-                             recs_per_state=sh["rps"], lanes=lanes, stream=sp)
+                             recs_per_state=sh["rps"], lanes=lanes, stream=sp, **ad_kw)
 
     def open_(b):
         _, ct, back, st = sets[b]
@@ -239,7 +275,7 @@ def main():
                              inp=ct.data_ptr(), out=back.data_ptr(), in_stride=out_stride,
                              out_stride=in_stride, length=L, n_records=N,
                              recs_per_state=sh["rps"], status=st.data_ptr(), lanes=lanes,
-                             stream=sp)
+                             stream=sp, **ad_kw)
 
     for w in range(args.warmup):
         assert seal(w % args.sets) == 0
@@ -281,12 +317,14 @@ def main():
 
     payload_step = 2.0 * N * L * world                         # both directions, all ranks
     value = payload_step * args.steps / elapsed / GIB
-    alg_seal = N * (2 * L + 16) + len(sh["key_ids"]) * 40       # SURVEY §8d algorithmic bytes
+    alg_seal = N * (2 * L + 16 + AD) + len(sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
     achieved = alg_seal / (seal_ms * 1e-3) / 1e9
     kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L)
-    traffic = load_traffic(args.config, kname)
+    pmc = load_pmc(args.config, kname)
+    traffic = pmc.get("hbm_bytes_per_launch")
     result = {
-        "metric": "GiB/s device-resident AEAD encrypt+decrypt, 64Ki x 1400B records per GPU",
+        "metric": (f"GiB/s device-resident AEAD encrypt+decrypt, {N // 1024}Ki x {L}B records"
+                   + (f" + {AD}B AD" if AD else "") + " per GPU"),
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -306,7 +344,8 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": kname,
                      "algorithmic_bytes_per_launch": alg_seal,
-                     "avg_launch_ms": round(seal_ms, 5)},
+                     "avg_launch_ms": round(seal_ms, 5),
+                     "issue_bound": issue_bound(pmc, seal_ms)},
         "seal_gibs": round(N * L * world / (seal_ms * 1e-3) / GIB, 2),
         "open_gibs": round(N * L * world / (open_ms * 1e-3) / GIB, 2),
         "open_roofline_frac": round(alg_seal / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

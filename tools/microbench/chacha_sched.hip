@@ -84,8 +84,8 @@ __device__ __forceinline__ void dround(uint32_t s[16]) {
 }
 
 constexpr int NB = 64;
-template <int V>
-__global__ void __launch_bounds__(256) kchacha(uint32_t *o, uint32_t seed) {
+template <int V, int SYNC = 0, int BS = 256>
+__global__ void __launch_bounds__(BS) kchacha(uint32_t *o, uint32_t seed) {
   uint32_t x[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) x[i] = seed * (i + 1) + threadIdx.x + blockIdx.x * 977u;
@@ -95,12 +95,15 @@ __global__ void __launch_bounds__(256) kchacha(uint32_t *o, uint32_t seed) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) s[i] = x[i];
 #pragma unroll 2
-    for (int r = 0; r < 10; ++r) dround<V>(s);
+    for (int r = 0; r < 10; ++r) {
+      dround<V>(s);
+      if (SYNC) __syncthreads();
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc ^= s[i] + x[i];
     x[12] += 1;
   }
-  o[blockIdx.x * 256 + threadIdx.x] = acc;
+  o[blockIdx.x * BS + threadIdx.x] = acc;
 }
 
 int main() {
@@ -126,6 +129,27 @@ int main() {
     (void)hipMemcpy(h[vi], d, 256 * 4, hipMemcpyDeviceToHost);
   };
   run(kchacha<0>, 0); run(kchacha<1>, 1); run(kchacha<2>, 2); run(kchacha<3>, 3);
+  // lock-step waves: a workgroup of W waves per SIMD (BS = 256*W), barrier per double round
+  auto run2 = [&](auto k, const char *name, int bs) {
+    int wps = bs / 256;
+    for (int rounds = 1; rounds <= 2; ++rounds) {
+      int blocks = cus * rounds;   // rounds x wps waves per SIMD
+      hipLaunchKernelGGL(k, dim3(blocks), dim3(bs), 0, 0, d, 5u); (void)hipDeviceSynchronize();
+      (void)hipEventRecord(e0);
+      for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(k, dim3(blocks), dim3(bs), 0, 0, d, 5u);
+      (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+      float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+      double wave_blocks = 3.0 * blocks * (bs / 64) * NB;
+      double cyc = (ms * 1e-3) * 2.4e9 * cus * 4 / wave_blocks;
+      printf("%-26s waves/SIMD %d  %7.1f SIMD-cyc/wave-block(@2.4GHz)\n", name, wps * rounds, cyc);
+    }
+  };
+  run2(kchacha<0, 0, 512>, "compiler bs512 nosync", 512);
+  run2(kchacha<0, 1, 512>, "compiler bs512 sync/dr", 512);
+  run2(kchacha<1, 1, 512>, "grouped bs512 sync/dr", 512);
+  run2(kchacha<0, 0, 1024>, "compiler bs1024 nosync", 1024);
+  run2(kchacha<0, 1, 1024>, "compiler bs1024 sync/dr", 1024);
+  run2(kchacha<1, 1, 1024>, "grouped bs1024 sync/dr", 1024);
   int ok = 1;
   for (int v = 1; v < 4; ++v) for (int i = 0; i < 256; ++i) ok &= h[v][i] == h[0][i];
   printf("variants agree: %s\n", ok ? "yes" : "NO");
