@@ -204,7 +204,14 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
     if (cipher_id == NOISE_CIPHER_AESGCM) {
         int rc = hip_rc(ensure_aes_tables(s));
         if (rc) return rc;
-        return launch(open ? gcm_ragged<true> : gcm_ragged<false>, job->n_records, GCM_LANES, a, s);
+        if (job->n_records == 0) return NOISE_ERROR_NONE;
+        /* LDS-staged kernel: 1024-thread workgroups over 256-record windows */
+        const bool fast = (job->flags & NOISE_AEAD_FLAG_FAST) != 0;
+        const uint32_t blocks = (job->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
+        KernelFn<RaggedArgs> fn = open ? (fast ? gcm_ragged_staged<true, true> : gcm_ragged_staged<true, false>)
+                                       : (fast ? gcm_ragged_staged<false, true> : gcm_ragged_staged<false, false>);
+        hipLaunchKernelGGL(fn, dim3(blocks), dim3(GCM_WG), 0, s, a);
+        return hip_rc(hipGetLastError());
     }
     return NOISE_ERROR_UNKNOWN_ID;
 }

@@ -4,6 +4,7 @@
  * include/noise_aead_hip.h.
  */
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace na {
@@ -44,6 +45,43 @@ struct RaggedArgs {
     uint8_t *status;
     uint32_t n_records;
 };
+
+/* Length-balanced record order for a workgroup of a ragged batch.  A wave is
+   as slow as its longest record, so the NREC records of the workgroup's
+   window [base, base + NREC) are ranked by length (bitonic sort of
+   len << 8 | index in LDS, every thread of the workgroup taking part) and
+   record group g takes the g-th: the records sharing a wave then have
+   near-equal lengths.  The result is a permutation of the window, so every
+   record is still processed exactly once.  Returns the record of group g, or
+   UINT32_MAX past the batch end.  Must be reached by the whole workgroup. */
+template <int NREC>
+__device__ __forceinline__ uint32_t window_rec(const RecDesc *recs, uint32_t n, uint32_t base,
+                                               uint32_t g, uint32_t *keys)
+{
+    static_assert(NREC >= 2 && NREC <= 256 && (NREC & (NREC - 1)) == 0, "window");
+    const uint32_t t = threadIdx.x, nt = blockDim.x;
+    for (uint32_t i = t; i < (uint32_t)NREC; i += nt) {
+        const uint32_t rec = base + i;
+        keys[i] = rec < n ? (recs[rec].len << 8) | i : 0xFFFFFFFFu; /* len <= 65519 */
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= (uint32_t)NREC; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = t; i < (uint32_t)NREC; i += nt) {
+                const uint32_t p = i ^ j;
+                if (p > i) {
+                    const uint32_t x = keys[i], y = keys[p];
+                    if ((x > y) == ((i & k) == 0)) {
+                        keys[i] = y;
+                        keys[p] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    const uint32_t key = keys[g < (uint32_t)NREC ? g : 0];
+    return (g < (uint32_t)NREC && key != 0xFFFFFFFFu) ? base + (key & 0xFFu) : 0xFFFFFFFFu;
+}
 
 /* AES-GCM per-state device context (prepared once per key). */
 constexpr int GCM_LANES = 4;                    /* lanes per record */

@@ -351,11 +351,13 @@ template <bool OPEN>
 __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
 {
     __shared__ uint32_t te[256], sb[256];
+    __shared__ uint32_t order[256 / GCM_LANES];
     load_aes_tables(te, sb);
-    const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t rec = gtid / GCM_LANES;
+    const uint32_t rec = window_rec<256 / GCM_LANES>(a.recs, a.n_records,
+                                                     blockIdx.x * (256u / GCM_LANES),
+                                                     threadIdx.x / GCM_LANES, order);
     if (rec >= a.n_records) return;
-    const int l = (int)(gtid % GCM_LANES);
+    const int l = (int)(threadIdx.x % GCM_LANES);
     const RecDesc d = a.recs[rec];
     GcmView rv;
     rv.src = a.in + d.in_off;
@@ -410,21 +412,21 @@ NA_DEV void gcm_lds_fill(GcmLds &L, const AesCtx *ctx)
     __syncthreads();
 }
 
+/* te: the LDS base of the replicated Te0|Te1, Te2|Te3 regions (GcmLds::te) */
 template <int TAB, int K>
-NA_DEV uint32_t te_lookup(const GcmLds &L, uint32_t s, uint32_t lane_tpl)
+NA_DEV uint32_t te_lookup(const uint8_t *te, uint32_t s, uint32_t lane_tpl)
 {
     /* perm: out byte0 = tpl byte0 (4c) or byte1 (128 + 4c) for Te1/Te3,
        byte1 = s byte K, byte2 = tpl byte2 (1) for Te2/Te3 else 0, byte3 = 0 */
     constexpr uint32_t sel = (0x0cu << 24) | ((TAB >= 2 ? 2u : 0x0cu) << 16) | ((4u + K) << 8) |
                              (TAB & 1 ? 1u : 0u);
     const uint32_t addr = __builtin_amdgcn_perm(s, lane_tpl, sel);
-    return *(const uint32_t *)((const uint8_t *)&L.te[0][0][0] + addr);
+    return *(const uint32_t *)(te + addr);
 }
 
-NA_DEV void aes256_lds(const GcmLds &L, uint32_t tpl, uint32_t &s0, uint32_t &s1, uint32_t &s2,
-                       uint32_t &s3)
+NA_DEV void aes256_lds(const uint8_t *L, const uint32_t *rk, uint32_t tpl, uint32_t &s0,
+                       uint32_t &s1, uint32_t &s2, uint32_t &s3)
 {
-    const uint32_t *rk = L.rk;
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
@@ -451,11 +453,11 @@ NA_DEV void aes256_lds(const GcmLds &L, uint32_t tpl, uint32_t &s0, uint32_t &s1
     s0 = o0 ^ rk[56]; s1 = o1 ^ rk[57]; s2 = o2 ^ rk[58]; s3 = o3 ^ rk[59];
 }
 
-NA_DEV void aes_ctr_lds(const GcmLds &L, uint32_t tpl, uint32_t n_hi, uint32_t n_lo, uint32_t ctr,
-                        uint32_t ks[4])
+NA_DEV void aes_ctr_lds(const uint8_t *te, const uint32_t *rk, uint32_t tpl, uint32_t n_hi,
+                        uint32_t n_lo, uint32_t ctr, uint32_t ks[4])
 {
     uint32_t s0 = 0, s1 = n_hi, s2 = n_lo, s3 = ctr;
-    aes256_lds(L, tpl, s0, s1, s2, s3);
+    aes256_lds(te, rk, tpl, s0, s1, s2, s3);
     ks[0] = __builtin_bswap32(s0); ks[1] = __builtin_bswap32(s1);
     ks[2] = __builtin_bswap32(s2); ks[3] = __builtin_bswap32(s3);
 }
@@ -472,6 +474,7 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
 {
     constexpr int K = GCM_LANES;
     __shared__ GcmLds L;
+    const uint8_t *TE = (const uint8_t *)&L.te[0][0][0];
     const uint32_t rec0 = blockIdx.x * (uint32_t)GCM_WG_RECS;
     const uint32_t st = rec0 / a.rps; /* one state per workgroup (host-checked) */
     const AesCtx *ctx = (const AesCtx *)a.keys + st;
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
             const uint32_t nb = min(len - 16 * d, 16u);
             if (!OPEN) {
                 uint32_t ks[4];
-                aes_ctr_lds(L, tpl, n_hi, n_lo, 2 + d, ks);
+                aes_ctr_lds(TE, L.rk, tpl, n_hi, n_lo, 2 + d, ks);
 #pragma unroll
                 for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
                 if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
@@ -531,7 +534,7 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
     uint32_t ej[4];
-    aes_ctr_lds(L, tpl, n_hi, n_lo, 1u, ej);
+    aes_ctr_lds(TE, L.rk, tpl, n_hi, n_lo, 1u, ej);
     const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
     if (!OPEN) {
         if (l == K - 1) {
@@ -551,7 +554,7 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
     for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
         const uint4 v = *(const uint4 *)(src + 16 * d);
         uint32_t x[4] = {v.x, v.y, v.z, v.w}, ks[4];
-        aes_ctr_lds(L, tpl, n_hi, n_lo, 2 + d, ks);
+        aes_ctr_lds(TE, L.rk, tpl, n_hi, n_lo, 2 + d, ks);
 #pragma unroll
         for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
         const uint32_t nb = min(len - 16 * d, 16u);
@@ -560,4 +563,160 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
     }
 }
 
+/* ------------------------------ staged ragged (any mix of states / lengths)
+ *
+ * 1024-thread workgroups over windows of 256 descriptors, with the same
+ * replicated LDS T-tables as gcm_staged.  A ragged window may mix states, so
+ * the GHASH Horner table and the round keys of up to two states are staged
+ * in LDS slots (the states of the window's first and last records: a window
+ * that spans a run boundary of per-state records holds exactly these two);
+ * a record of any other state reads its own context from global memory.
+ * Records are taken in length order inside the window (window_rec) so the
+ * 16 records of a wave have near-equal lengths.
+ */
+struct GcmLdsR {
+    uint32_t te[2][256][64];
+    uint4 h4[2][GHASH_TAB_ENTRIES];
+    uint32_t rk[2][60];
+    uint32_t order[GCM_WG_RECS];
+};
+
+/* One record, 4 lanes (l = 0..3): gcm_staged's GHASH/CTR core with the
+   record's tables passed in; FAST as in chachapoly.hip (16-B aligned record,
+   input readable to roundup16). */
+template <bool OPEN, bool FAST>
+NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint32_t tpl,
+                              const uint32_t *rk, const uint4 *h4)
+{
+    constexpr int K = GCM_LANES;
+    const uint32_t n_hi = (uint32_t)(rv.nonce >> 32), n_lo = (uint32_t)rv.nonce;
+    const uint32_t len = rv.len, ad_len = rv.ad_len;
+    const uint32_t A = (ad_len + 15) / 16, M = (len + 15) / 16;
+    const uint32_t n = A + M + 1;
+    const uint32_t c0 = ((uint32_t)l + n) % K;
+    uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll 1
+    for (uint32_t i = c0; i < n; i += K) {
+        if (i != c0) gh_mul_lds<OPEN>(acc, h4);
+        uint32_t x[4];
+        if (i >= A && i < A + M) {
+            const uint32_t d = i - A;
+            const uint32_t nb = min(len - 16 * d, 16u);
+            if (FAST) {
+                const uint4 v = *(const uint4 *)(rv.src + 16 * d);
+                x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+            } else {
+                load16(rv.src + 16 * d, nb, x);
+            }
+            if (!OPEN) {
+                uint32_t ks[4];
+                aes_ctr_lds(TE, rk, tpl, n_hi, n_lo, 2 + d, ks);
+#pragma unroll
+                for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+                if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
+                else store16(rv.dst + 16 * d, nb, x);
+            }
+#pragma unroll
+            for (int w = 0; w < 4; ++w) x[w] &= blk_mask(nb, w);
+        } else if (i < A) {
+            const uint32_t rem = ad_len - 16 * i;
+            load16(rv.ad + 16 * i, rem >= 16 ? 16u : rem, x);
+        } else {
+            const uint64_t ab = (uint64_t)ad_len * 8, cb = (uint64_t)len * 8;
+            x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
+            x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
+        }
+        acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
+    }
+    gh_mul(acc, (const uint4 *)rv.ctx->tab[K - 1 - l]);
+#pragma unroll
+    for (int off = 1; off < K; off <<= 1)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+    uint32_t ej[4];
+    aes_ctr_lds(TE, rk, tpl, n_hi, n_lo, 1u, ej);
+    const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
+    if (!OPEN) {
+        if (l == K - 1) store16(rv.dst + len, 16, tag);
+        return true;
+    }
+    uint32_t got[4];
+    load16(rv.src + len, 16, got);
+    const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) == 0;
+    if (!ok) return false; /* cipher-aesgcm.c:184-186: nothing decrypted */
+    for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
+        const uint32_t nb = min(len - 16 * d, 16u);
+        uint32_t x[4], ks[4];
+        if (FAST) {
+            const uint4 v = *(const uint4 *)(rv.src + 16 * d);
+            x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+        } else {
+            load16(rv.src + 16 * d, nb, x);
+        }
+        aes_ctr_lds(TE, rk, tpl, n_hi, n_lo, 2 + d, ks);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+        if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
+        else store16(rv.dst + 16 * d, nb, x);
+    }
+    return true;
+}
+
+/* the cold path: a record whose state has no LDS slot (kept out of line so
+   its register needs do not weigh on the slot path) */
+template <bool OPEN, bool FAST>
+__device__ __attribute__((noinline)) bool gcm_record_global(const GcmView &rv, int l,
+                                                            const uint8_t *TE, uint32_t tpl)
+{
+    return gcm_record_staged<OPEN, FAST>(rv, l, TE, tpl, rv.ctx->rk,
+                                         (const uint4 *)rv.ctx->tab[GCM_LANES - 1]);
+}
+
+template <bool OPEN, bool FAST>
+__global__ __launch_bounds__(GCM_WG) void gcm_ragged_staged(RaggedArgs a)
+{
+    constexpr int K = GCM_LANES;
+    __shared__ GcmLdsR L;
+    const uint8_t *TE = (const uint8_t *)&L.te[0][0][0];
+    const uint32_t base = blockIdx.x * (uint32_t)GCM_WG_RECS;
+    const uint32_t last = min(base + (uint32_t)GCM_WG_RECS, a.n_records) - 1;
+    const uint64_t slot_off[2] = {a.recs[base].ctx_off, a.recs[last].ctx_off};
+    /* T-tables (as gcm_lds_fill) and the two slots' tables */
+    for (int q = threadIdx.x; q < 2 * 256 * 16; q += GCM_WG) {
+        const int reg = q >> 12, row = (q >> 4) & 255, quad = q & 15;
+        const int tab = 2 * reg + (quad >> 3);
+        const uint32_t v = rotr(g_te0[row], 8 * tab);
+        ((uint4 *)&L.te[reg][row][0])[quad] = make_uint4(v, v, v, v);
+    }
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+        const AesCtx *ctx = (const AesCtx *)(a.keys + slot_off[sl]);
+        const uint4 *src = (const uint4 *)ctx->tab[K - 1];
+        for (int i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += GCM_WG) L.h4[sl][i] = src[i];
+        if (threadIdx.x < 60) L.rk[sl][threadIdx.x] = ctx->rk[threadIdx.x];
+    }
+    const uint32_t rec = window_rec<GCM_WG_RECS>(a.recs, a.n_records, base, threadIdx.x / K, L.order);
+    if (rec >= a.n_records) return;
+    const int l = (int)(threadIdx.x % K);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t tpl = (1u << 16) | ((128u + 4u * (lane & 31)) << 8) | (4u * (lane & 31));
+    const RecDesc d = a.recs[rec];
+    GcmView rv;
+    rv.src = a.in + d.in_off;
+    rv.dst = a.out + d.out_off;
+    rv.ad = a.ad ? a.ad + d.ad_off : nullptr;
+    rv.ctx = (const AesCtx *)(a.keys + d.ctx_off);
+    rv.nonce = d.nonce;
+    rv.len = d.len;
+    rv.ad_len = d.ad_len;
+    bool ok;
+    const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
+    if (sl >= 0)
+        ok = gcm_record_staged<OPEN, FAST>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
+    else /* a third state in the window: its own context, from global memory */
+        ok = gcm_record_global<OPEN, FAST>(rv, l, TE, tpl);
+    if (OPEN && l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+}
+
 } // namespace na
+

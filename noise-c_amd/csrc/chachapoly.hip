@@ -1068,22 +1068,26 @@ __global__ __launch_bounds__(256) void chachapoly_open_uniform(UniformArgs a)
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
+/* Ragged batches: the workgroup's 256/K records are taken in length order
+   (window_rec), so the records sharing a wave have near-equal lengths. */
 template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_seal_ragged(RaggedArgs a)
 {
-    const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t rec = gtid / K;
+    __shared__ uint32_t order[256 / K];
+    const uint32_t rec = window_rec<256 / K>(a.recs, a.n_records, blockIdx.x * (256u / K),
+                                             threadIdx.x / K, order);
     if (rec >= a.n_records) return;
-    seal_any<K, FAST>(ragged_view(a, rec), (int)(gtid % K));
+    seal_any<K, FAST>(ragged_view(a, rec), (int)(threadIdx.x % K));
 }
 
 template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
 {
-    const uint32_t gtid = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t rec = gtid / K;
+    __shared__ uint32_t order[256 / K];
+    const uint32_t rec = window_rec<256 / K>(a.recs, a.n_records, blockIdx.x * (256u / K),
+                                             threadIdx.x / K, order);
     if (rec >= a.n_records) return;
-    const int k = (int)(gtid % K);
+    const int k = (int)(threadIdx.x % K);
     const bool ok = open_any<K, FAST>(ragged_view(a, rec), k);
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
