@@ -519,7 +519,12 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     ms, g, open_ = max(per, key=lambda x: x[0])
     alg = 2 * g["bytes"] + 16 * g["n"] + 40 * g["states"]
     achieved = alg / (ms * 1e-3) / 1e9
-    kname = ("chachapoly_" if g["cipher"] == CHACHA else "gcm_") + ("open" if open_ else "seal") + "_ragged"
+    # the kernel the library dispatches (aead_api.hip run_ragged), as rocprofv3 names it
+    if g["cipher"] == CHACHA:
+        kname = f"chachapoly_{'open' if open_ else 'seal'}_ragged<{args.lanes or 4}, true>"
+    else:
+        kname = f"gcm_ragged_staged<{'true' if open_ else 'false'}, true>"
+    pmc = load_pmc("c5", kname)
     result = {
         "metric": "GiB/s device-resident AEAD encrypt+decrypt, mixed 64B-16KiB records per GPU",
         "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -530,9 +535,10 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                    "states_per_gpu": S, "payload_bytes_per_step": int(2 * payload * world),
                    "parallelism": f"states x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc.get("hbm_bytes_per_launch"),
                      "kernel": kname, "algorithmic_bytes_per_launch": alg,
-                     "avg_launch_ms": round(ms, 5)},
+                     "avg_launch_ms": round(ms, 5), "issue_bound": issue_bound(pmc, ms)},
         "kernels_ms": {(("chacha" if gg["cipher"] == CHACHA else "aes") + ("_open" if o else "_seal")): round(m, 4)
                        for m, gg, o in per},
         "all_tags_verified": ok,
