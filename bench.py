@@ -523,7 +523,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     if g["cipher"] == CHACHA:
         kname = f"chachapoly_{'open' if open_ else 'seal'}_ragged<{args.lanes or 4}, true>"
     else:
-        kname = f"gcm_ragged_staged<{'true' if open_ else 'false'}, true>"
+        kname = f"gcm_ragged_staged<{'true' if open_ else 'false'}, true, 1024>"
     pmc = load_pmc("c5", kname)
     result = {
         "metric": "GiB/s device-resident AEAD encrypt+decrypt, mixed 64B-16KiB records per GPU",

@@ -205,12 +205,21 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
         int rc = hip_rc(ensure_aes_tables(s));
         if (rc) return rc;
         if (job->n_records == 0) return NOISE_ERROR_NONE;
-        /* LDS-staged kernel: 1024-thread workgroups over 256-record windows */
+        /* LDS-staged kernel: 1024-thread workgroups over 256-record windows;
+           a batch too small to give every CU one of those uses 256-thread
+           workgroups over 64-record windows instead (4x the workgroups) */
         const bool fast = (job->flags & NOISE_AEAD_FLAG_FAST) != 0;
-        const uint32_t blocks = (job->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
-        KernelFn<RaggedArgs> fn = open ? (fast ? gcm_ragged_staged<true, true> : gcm_ragged_staged<true, false>)
-                                       : (fast ? gcm_ragged_staged<false, true> : gcm_ragged_staged<false, false>);
-        hipLaunchKernelGGL(fn, dim3(blocks), dim3(GCM_WG), 0, s, a);
+        const bool big = job->n_records >= 256u * GCM_WG_RECS;
+        const uint32_t per = big ? GCM_WG_RECS : GCM_WG_RECS / 4;
+        const uint32_t blocks = (job->n_records + per - 1) / per;
+        KernelFn<RaggedArgs> fn;
+        if (big)
+            fn = open ? (fast ? gcm_ragged_staged<true, true, 1024> : gcm_ragged_staged<true, false, 1024>)
+                      : (fast ? gcm_ragged_staged<false, true, 1024> : gcm_ragged_staged<false, false, 1024>);
+        else
+            fn = open ? (fast ? gcm_ragged_staged<true, true, 256> : gcm_ragged_staged<true, false, 256>)
+                      : (fast ? gcm_ragged_staged<false, true, 256> : gcm_ragged_staged<false, false, 256>);
+        hipLaunchKernelGGL(fn, dim3(blocks), dim3(big ? 1024 : 256), 0, s, a);
         return hip_rc(hipGetLastError());
     }
     return NOISE_ERROR_UNKNOWN_ID;

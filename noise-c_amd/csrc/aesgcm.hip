@@ -574,11 +574,12 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
  * Records are taken in length order inside the window (window_rec) so the
  * 16 records of a wave have near-equal lengths.
  */
+template <int NREC>
 struct GcmLdsR {
     uint32_t te[2][256][64];
     uint4 h4[2][GHASH_TAB_ENTRIES];
     uint32_t rk[2][60];
-    uint32_t order[GCM_WG_RECS];
+    uint32_t order[NREC];
 };
 
 /* One record, 4 lanes (l = 0..3): gcm_staged's GHASH/CTR core with the
@@ -672,17 +673,19 @@ __device__ __attribute__((noinline)) bool gcm_record_global(const GcmView &rv, i
                                          (const uint4 *)rv.ctx->tab[GCM_LANES - 1]);
 }
 
-template <bool OPEN, bool FAST>
-__global__ __launch_bounds__(GCM_WG) void gcm_ragged_staged(RaggedArgs a)
+/* WG threads per workgroup (1024, or 256 for batches too small to give
+   every CU a 1024-thread workgroup); WG / 4 records per window */
+template <bool OPEN, bool FAST, int WG>
+__global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
 {
-    constexpr int K = GCM_LANES;
-    __shared__ GcmLdsR L;
+    constexpr int K = GCM_LANES, NREC = WG / GCM_LANES;
+    __shared__ GcmLdsR<NREC> L;
     const uint8_t *TE = (const uint8_t *)&L.te[0][0][0];
-    const uint32_t base = blockIdx.x * (uint32_t)GCM_WG_RECS;
-    const uint32_t last = min(base + (uint32_t)GCM_WG_RECS, a.n_records) - 1;
+    const uint32_t base = blockIdx.x * (uint32_t)NREC;
+    const uint32_t last = min(base + (uint32_t)NREC, a.n_records) - 1;
     const uint64_t slot_off[2] = {a.recs[base].ctx_off, a.recs[last].ctx_off};
     /* T-tables (as gcm_lds_fill) and the two slots' tables */
-    for (int q = threadIdx.x; q < 2 * 256 * 16; q += GCM_WG) {
+    for (int q = threadIdx.x; q < 2 * 256 * 16; q += WG) {
         const int reg = q >> 12, row = (q >> 4) & 255, quad = q & 15;
         const int tab = 2 * reg + (quad >> 3);
         const uint32_t v = rotr(g_te0[row], 8 * tab);
@@ -692,10 +695,10 @@ __global__ __launch_bounds__(GCM_WG) void gcm_ragged_staged(RaggedArgs a)
     for (int sl = 0; sl < 2; ++sl) {
         const AesCtx *ctx = (const AesCtx *)(a.keys + slot_off[sl]);
         const uint4 *src = (const uint4 *)ctx->tab[K - 1];
-        for (int i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += GCM_WG) L.h4[sl][i] = src[i];
+        for (int i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += WG) L.h4[sl][i] = src[i];
         if (threadIdx.x < 60) L.rk[sl][threadIdx.x] = ctx->rk[threadIdx.x];
     }
-    const uint32_t rec = window_rec<GCM_WG_RECS>(a.recs, a.n_records, base, threadIdx.x / K, L.order);
+    const uint32_t rec = window_rec<NREC>(a.recs, a.n_records, base, threadIdx.x / K, L.order);
     if (rec >= a.n_records) return;
     const int l = (int)(threadIdx.x % K);
     const uint32_t lane = threadIdx.x & 63;
