@@ -55,6 +55,14 @@ CONFIGS = {
                         "ragged descriptors"),
 }
 SEED_LEN, SEED_PT, SEED_KEY = 0x6C656E, 0x7074, 0x6B6579
+# NOISE_BENCH_REHEARSE=1: rehearse the N>1 code path on a one-GPU box — every
+# rank on cuda:0, gloo process group, collectives on CPU copies.  Only the
+# transport differs from the real run (RCCL refuses two ranks on one GPU).
+REHEARSE = os.environ.get("NOISE_BENCH_REHEARSE") == "1"
+
+
+def cpu_if_rehearsal(t):
+    return t.cpu() if REHEARSE else t
 IN_ALIGN = 16  # device record strides are padded to 16 B (layout)
 
 
@@ -215,10 +223,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if REHEARSE:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if REHEARSE:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -299,7 +312,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = cpu_if_rehearsal(torch.tensor([elapsed], dtype=torch.float64, device=dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
@@ -392,25 +405,36 @@ def xfer_leg(args, torch, dist, dev, A, rank, world, N, L, in_stride, out_stride
         torch.cuda.synchronize(dev)
         dist.barrier()
         t0 = time.perf_counter()
-        scatter_records(local_in, full_in, src=0)
+        if REHEARSE:  # gloo scatters CPU tensors
+            tmp = torch.empty(shard_in, dtype=torch.uint8)
+            scatter_records(tmp, full_in.cpu() if rank == 0 else None, src=0)
+            local_in.copy_(tmp)
+        else:
+            scatter_records(local_in, full_in, src=0)
         torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         if seal(0, local_in, local_out):
             raise RuntimeError("seal launch failed")
         torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
-        gather_records(local_out, full_out, dst=0)
+        if REHEARSE:
+            tmp = torch.empty(world * shard_out, dtype=torch.uint8) if rank == 0 else None
+            gather_records(local_out.cpu(), tmp, dst=0)
+            if rank == 0:
+                full_out.copy_(tmp)
+        else:
+            gather_records(local_out, full_out, dst=0)
         torch.cuda.synchronize(dev)
         t3 = time.perf_counter()
         if rep:  # rep 0 warms RCCL's channels
             phases.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0))
-    ph = torch.tensor(phases, dtype=torch.float64, device=dev).mean(0)
+    ph = cpu_if_rehearsal(torch.tensor(phases, dtype=torch.float64, device=dev).mean(0))
     dist.all_reduce(ph, op=dist.ReduceOp.MAX)
     # checks: scattered shard == this rank's own input; gathered shard g ==
     # rank g's sealed output (int64 checksums, all_gathered)
-    ok = torch.tensor([1 if torch.equal(local_in, sets[0][0]) else 0], device=dev)
+    ok = cpu_if_rehearsal(torch.tensor([1 if torch.equal(local_in, sets[0][0]) else 0], device=dev))
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    mine = local_out.view(torch.int64).sum().reshape(1)
+    mine = cpu_if_rehearsal(local_out.view(torch.int64).sum().reshape(1))
     sums = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(sums, mine)
     good = bool(ok.item())
@@ -419,7 +443,9 @@ def xfer_leg(args, torch, dist, dev, A, rank, world, N, L, in_stride, out_stride
             got = full_out[g * shard_out:(g + 1) * shard_out].view(torch.int64).sum()
             good &= bool(got.item() == sums[g].item())
     sc, se, ga, tot = (float(x) * 1e3 for x in ph.tolist())
-    return {"collective": "torch.distributed scatter/gather on nccl (RCCL grouped send/recv over xGMI)",
+    return {"collective": ("torch.distributed scatter/gather on gloo via host memory (one-GPU rehearsal)"
+                           if REHEARSE else
+                           "torch.distributed scatter/gather on nccl (RCCL grouped send/recv over xGMI)"),
             "src_dst_rank": 0, "shard_in_bytes": shard_in, "shard_out_bytes": shard_out,
             "scatter_ms": round(sc, 4), "seal_ms": round(se, 4), "gather_ms": round(ga, 4),
             "total_ms": round(tot, 4),
@@ -493,7 +519,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = cpu_if_rehearsal(torch.tensor([elapsed], dtype=torch.float64, device=dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
