@@ -462,6 +462,76 @@ NA_DEV void aes_ctr_lds(const uint8_t *te, const uint32_t *rk, uint32_t tpl, uin
     ks[2] = __builtin_bswap32(s2); ks[3] = __builtin_bswap32(s3);
 }
 
+/* Counter-mode caching.  Within one record the CTR input blocks
+   0^32 || BE64(n) || BE32(ctr) differ only in ctr, and ctr <= 4097 (a record
+   is at most 65519 bytes, the 16-bit counter rule of cipher-aesgcm.c:105-112)
+   so only the two low bytes of state word 3 vary.  After the first round two
+   of the four columns are constant and the other two each have one varying
+   lookup; in the second round 8 of the 16 lookups read those constant
+   columns.  AesPre holds the constant parts, computed once per record:
+   22 of a block's 240 table lookups are then done once per record instead
+   of once per block. */
+struct AesPre {
+    uint32_t c0, c1;         /* round 1, columns 0 and 1 without their ctr lookup */
+    uint32_t d0, d1, d2, d3; /* round 2, each column's two constant lookups + key */
+};
+
+NA_DEV AesPre aes_pre_lds(const uint8_t *L, const uint32_t *rk, uint32_t tpl, uint32_t n_hi,
+                          uint32_t n_lo)
+{
+    const uint32_t s0 = rk[0], s1 = n_hi ^ rk[1], s2 = n_lo ^ rk[2], s3 = rk[3];
+    AesPre p;
+    p.c0 = xor3(te_lookup<0, 3>(L, s0, tpl), te_lookup<1, 2>(L, s1, tpl),
+                te_lookup<2, 1>(L, s2, tpl)) ^ rk[4];
+    p.c1 = xor3(te_lookup<0, 3>(L, s1, tpl), te_lookup<1, 2>(L, s2, tpl),
+                te_lookup<3, 0>(L, s0, tpl)) ^ rk[5];
+    /* s3's bytes 2 and 3 are rk[3]'s: ctr < 2^16 */
+    const uint32_t t2 = xor3(xor3(te_lookup<0, 3>(L, s2, tpl), te_lookup<1, 2>(L, s3, tpl),
+                                  te_lookup<2, 1>(L, s0, tpl)), te_lookup<3, 0>(L, s1, tpl), rk[6]);
+    const uint32_t t3 = xor3(xor3(te_lookup<0, 3>(L, s3, tpl), te_lookup<1, 2>(L, s0, tpl),
+                                  te_lookup<2, 1>(L, s1, tpl)), te_lookup<3, 0>(L, s2, tpl), rk[7]);
+    p.d0 = xor3(te_lookup<2, 1>(L, t2, tpl), te_lookup<3, 0>(L, t3, tpl), rk[8]);
+    p.d1 = xor3(te_lookup<1, 2>(L, t2, tpl), te_lookup<2, 1>(L, t3, tpl), rk[9]);
+    p.d2 = xor3(te_lookup<0, 3>(L, t2, tpl), te_lookup<1, 2>(L, t3, tpl), rk[10]);
+    p.d3 = xor3(te_lookup<0, 3>(L, t3, tpl), te_lookup<3, 0>(L, t2, tpl), rk[11]);
+    return p;
+}
+
+/* E_K(0^32 || BE64(n) || BE32(ctr)) from the record's AesPre (ctr < 2^16),
+   as little-endian memory words; equals aes_ctr_lds. */
+NA_DEV void aes_ctr_pre(const uint8_t *L, const uint32_t *rk, uint32_t tpl, const AesPre &p,
+                        uint32_t ctr, uint32_t ks[4])
+{
+    const uint32_t s3 = ctr ^ rk[3];
+    const uint32_t t0 = p.c0 ^ te_lookup<3, 0>(L, s3, tpl);
+    const uint32_t t1 = p.c1 ^ te_lookup<2, 1>(L, s3, tpl);
+    uint32_t s0 = xor3(p.d0, te_lookup<0, 3>(L, t0, tpl), te_lookup<1, 2>(L, t1, tpl));
+    uint32_t s1 = xor3(p.d1, te_lookup<0, 3>(L, t1, tpl), te_lookup<3, 0>(L, t0, tpl));
+    uint32_t s2 = xor3(p.d2, te_lookup<2, 1>(L, t0, tpl), te_lookup<3, 0>(L, t1, tpl));
+    uint32_t s3b = xor3(p.d3, te_lookup<1, 2>(L, t0, tpl), te_lookup<2, 1>(L, t1, tpl));
+#pragma unroll
+    for (int r = 3; r < 14; ++r) {
+#define NA_COL(a, b, c, d, k)                                                        \
+    xor3(xor3(te_lookup<0, 3>(L, a, tpl), te_lookup<1, 2>(L, b, tpl),                   \
+              te_lookup<2, 1>(L, c, tpl)),                                             \
+         te_lookup<3, 0>(L, d, tpl), rk[k])
+        const uint32_t u0 = NA_COL(s0, s1, s2, s3b, 4 * r);
+        const uint32_t u1 = NA_COL(s1, s2, s3b, s0, 4 * r + 1);
+        const uint32_t u2 = NA_COL(s2, s3b, s0, s1, 4 * r + 2);
+        const uint32_t u3 = NA_COL(s3b, s0, s1, s2, 4 * r + 3);
+#undef NA_COL
+        s0 = u0; s1 = u1; s2 = u2; s3b = u3;
+    }
+#define NA_SB4(a, b, c, d)                                                          \
+    ((te_lookup<2, 3>(L, a, tpl) & 0xff000000u) | (te_lookup<3, 2>(L, b, tpl) & 0x00ff0000u) | \
+     (te_lookup<0, 1>(L, c, tpl) & 0x0000ff00u) | (te_lookup<1, 0>(L, d, tpl) & 0x000000ffu))
+    const uint32_t o0 = NA_SB4(s0, s1, s2, s3b), o1 = NA_SB4(s1, s2, s3b, s0);
+    const uint32_t o2 = NA_SB4(s2, s3b, s0, s1), o3 = NA_SB4(s3b, s0, s1, s2);
+#undef NA_SB4
+    ks[0] = __builtin_bswap32(o0 ^ rk[56]); ks[1] = __builtin_bswap32(o1 ^ rk[57]);
+    ks[2] = __builtin_bswap32(o2 ^ rk[58]); ks[3] = __builtin_bswap32(o3 ^ rk[59]);
+}
+
 /* byte mask of the first nb (0..16) bytes of a 16-B block, word w */
 NA_DEV uint32_t blk_mask(uint32_t nb, int w)
 {
@@ -498,6 +568,8 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
 
     /* GHASH (and, sealing, CTR) over this lane's blocks i = c0, c0+K, ... */
     uint32_t acc[4] = {0, 0, 0, 0};
+    AesPre pre;
+    if (!OPEN) pre = aes_pre_lds(TE, L.rk, tpl, n_hi, n_lo);
 #pragma unroll 1
     for (uint32_t i = c0; i < n; i += K) {
         if (i != c0) gh_mul_lds<OPEN>(acc, L.h4);
@@ -509,7 +581,7 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
             const uint32_t nb = min(len - 16 * d, 16u);
             if (!OPEN) {
                 uint32_t ks[4];
-                aes_ctr_lds(TE, L.rk, tpl, n_hi, n_lo, 2 + d, ks);
+                aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
 #pragma unroll
                 for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
                 if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
@@ -533,8 +605,9 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
     for (int off = 1; off < K; off <<= 1)
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+    if (OPEN) pre = aes_pre_lds(TE, L.rk, tpl, n_hi, n_lo);
     uint32_t ej[4];
-    aes_ctr_lds(TE, L.rk, tpl, n_hi, n_lo, 1u, ej);
+    aes_ctr_pre(TE, L.rk, tpl, pre, 1u, ej);
     const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
     if (!OPEN) {
         if (l == K - 1) {
@@ -554,7 +627,7 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
     for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
         const uint4 v = *(const uint4 *)(src + 16 * d);
         uint32_t x[4] = {v.x, v.y, v.z, v.w}, ks[4];
-        aes_ctr_lds(TE, L.rk, tpl, n_hi, n_lo, 2 + d, ks);
+        aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
 #pragma unroll
         for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
         const uint32_t nb = min(len - 16 * d, 16u);
@@ -596,6 +669,8 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
     const uint32_t n = A + M + 1;
     const uint32_t c0 = ((uint32_t)l + n) % K;
     uint32_t acc[4] = {0, 0, 0, 0};
+    AesPre pre;
+    if (!OPEN) pre = aes_pre_lds(TE, rk, tpl, n_hi, n_lo);
 #pragma unroll 1
     for (uint32_t i = c0; i < n; i += K) {
         if (i != c0) gh_mul_lds<OPEN>(acc, h4);
@@ -611,7 +686,7 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
             }
             if (!OPEN) {
                 uint32_t ks[4];
-                aes_ctr_lds(TE, rk, tpl, n_hi, n_lo, 2 + d, ks);
+                aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
 #pragma unroll
                 for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
                 if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
@@ -634,8 +709,9 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
     for (int off = 1; off < K; off <<= 1)
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+    if (OPEN) pre = aes_pre_lds(TE, rk, tpl, n_hi, n_lo);
     uint32_t ej[4];
-    aes_ctr_lds(TE, rk, tpl, n_hi, n_lo, 1u, ej);
+    aes_ctr_pre(TE, rk, tpl, pre, 1u, ej);
     const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
     if (!OPEN) {
         if (l == K - 1) store16(rv.dst + len, 16, tag);
@@ -654,7 +730,7 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
         } else {
             load16(rv.src + 16 * d, nb, x);
         }
-        aes_ctr_lds(TE, rk, tpl, n_hi, n_lo, 2 + d, ks);
+        aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
 #pragma unroll
         for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
         if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
