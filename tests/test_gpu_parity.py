@@ -316,6 +316,75 @@ def test_ragged_vs_oracle(aead, gpu, oracle, cipher):
         assert np.array_equal(back[o: o + L], inp[io: io + L])
 
 
+@pytest.mark.parametrize("cipher", [CHACHA, AES])
+@pytest.mark.parametrize("fast", [True, False])
+def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, fast):
+    """Many workgroup windows (records taken in length order inside each),
+    per-state record runs of uneven size (so some windows hold 2 states,
+    some 3+: the AES LDS state slots and the global-context path), 1/2 of
+    the records in place, every 37th record tampered: each status, each
+    verified plaintext and each rejected record's untouched bytes must match
+    the oracle."""
+    torch = _torch()
+    rng = np.random.default_rng(77 + (cipher & 3) + 10 * fast)
+    count = 1500
+    runs = []
+    while sum(runs) < count:
+        runs.append(int(rng.choice([1, 3, 40, 130, 300])))
+    state_of = np.repeat(np.arange(len(runs)), runs)[:count]
+    S = len(runs)
+    keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
+    ctx, _k = prepare(aead, cipher, keys)
+    cb = aead.dev_ctx_bytes(cipher)
+    lens = rng.integers(0, 4000, count)
+    lens[::97] = 16384
+    slot = lambda L: ((int(L) + 16 + 63) // 64) * 64 if fast else int(L) + 16 + 5
+    offs = np.zeros(count, dtype=np.int64)
+    offs[1:] = np.cumsum([slot(L) for L in lens])[:-1]
+    total = int(offs[-1]) + slot(lens[-1]) + 64
+    pt = rng.integers(0, 256, total, dtype=np.uint8)
+    nonces = rng.integers(0, 2**62, count, dtype=np.int64).astype(np.uint64)
+    dt = [("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "<u8"),
+          ("ad_off", "<u8"), ("len", "<u4"), ("ad_len", "<u4")]
+    recs = np.zeros(count, dtype=dt)
+    recs["in_off"] = recs["out_off"] = offs
+    recs["nonce"] = nonces
+    recs["ctx_off"] = state_of.astype(np.uint64) * cb
+    recs["len"] = lens
+    d_recs = dev(recs.view(np.uint8))
+    d_buf = dev(pt)
+    flags = aead.FLAG_FAST if fast else 0
+    assert aead.dev_ragged(False, cipher, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
+                           inp=d_buf.data_ptr(), out=d_buf.data_ptr(), n_records=count,
+                           flags=flags, stream=stream()) == 0
+    sync()
+    sealed = d_buf.cpu().numpy().copy()
+    for i in list(range(0, count, 7)) + [count - 1]:
+        o, L = int(offs[i]), int(lens[i])
+        exp = oracle.encrypt(cipher, bytes(keys[state_of[i]]), int(nonces[i]), bytes(pt[o:o + L]))
+        assert bytes(sealed[o:o + L + 16]) == exp, i
+    bad = np.arange(count) % 37 == 5
+    tampered = sealed.copy()
+    for i in np.nonzero(bad)[0]:
+        o, L = int(offs[i]), int(lens[i])
+        tampered[o + L + int(rng.integers(0, 16))] ^= 0x40
+    d_buf = dev(tampered)
+    d_st = torch.full((count,), 9, dtype=torch.uint8, device="cuda")
+    assert aead.dev_ragged(True, cipher, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
+                           inp=d_buf.data_ptr(), out=d_buf.data_ptr(), n_records=count,
+                           status=d_st.data_ptr(), flags=flags, stream=stream()) == 0
+    sync()
+    st = d_st.cpu().numpy()
+    back = d_buf.cpu().numpy()
+    assert np.array_equal(st != 0, bad)
+    for i in range(count):
+        o, L = int(offs[i]), int(lens[i])
+        if bad[i]:
+            assert np.array_equal(back[o:o + L + 16], tampered[o:o + L + 16]), i
+        else:
+            assert np.array_equal(back[o:o + L], pt[o:o + L]), i
+
+
 # ------------------------------------------- the CipherState API on the GPU
 
 def test_golden_grid_through_cipherstate(aead, gpu, oracle, golden):
