@@ -56,6 +56,10 @@ typedef struct {
 #define NOISE_CIPHER_CATEGORY NOISE_ID('C', 0)
 #define NOISE_CIPHER_CHACHAPOLY NOISE_ID('C', 1)
 #define NOISE_CIPHER_AESGCM NOISE_ID('C', 2)
+#define NOISE_HASH_BLAKE2s NOISE_ID('H', 1) /* constants.h:43-46 */
+#define NOISE_HASH_BLAKE2b NOISE_ID('H', 2)
+#define NOISE_HASH_SHA256 NOISE_ID('H', 3)
+#define NOISE_HASH_SHA512 NOISE_ID('H', 4)
 #define NOISE_ERROR_NONE 0
 #define NOISE_ERROR_NO_MEMORY NOISE_ID('E', 1)
 #define NOISE_ERROR_UNKNOWN_ID NOISE_ID('E', 2)
@@ -233,6 +237,25 @@ typedef struct NoiseAeadRagged {
 
 int noise_aead_dev_seal_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);
 int noise_aead_dev_open_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);
+
+/* ------------------------------------------------ 5. session key fan-out
+ *
+ * SURVEY.md §8f rank 2.  For n sessions at once, the HKDF of
+ * noise_hashstate_hkdf (src/protocol/hashstate.c:476-516) with the session's
+ * Noise hash (NOISE_HASH_BLAKE2s/BLAKE2b/SHA256/SHA512):
+ *   out1[i] || out2[i] = HKDF(keys[i], data[i])   (each truncated)
+ * keys[i] = d_keys + i*key_len (1..256 bytes), data[i] = d_data + i*data_len
+ * (0..256 bytes; d_data may be NULL when data_len is 0), output lengths at
+ * most the hash length (NOISE_ERROR_INVALID_LENGTH otherwise, as
+ * hashstate.c:496-497).  noise_aead_dev_split is the key derivation of
+ * noise_symmetricstate_split (symmetricstate.c:530-533): HKDF(ck, "") into
+ * two 32-byte transport keys per session (ck is the hash length), ready for
+ * noise_aead_dev_prepare.  Device pointers, asynchronous on `stream`. */
+int noise_aead_dev_hkdf(int hash_id, const uint8_t *d_keys, uint32_t key_len,
+                        const uint8_t *d_data, uint32_t data_len, uint32_t n, uint8_t *d_out1,
+                        uint32_t out1_len, uint8_t *d_out2, uint32_t out2_len, void *stream);
+int noise_aead_dev_split(int hash_id, const uint8_t *d_ck, uint32_t n, uint8_t *d_k1,
+                         uint8_t *d_k2, void *stream);
 
 /* Default lanes per record the library picks for a batch of n records. */
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records);

@@ -14,6 +14,7 @@
 
 #include "chachapoly.hip"
 #include "aesgcm.hip"
+#include "kdf.hip"
 
 using namespace na;
 
@@ -306,6 +307,44 @@ int noise_aead_dev_fill_splitmix(uint8_t *d_out, uint64_t nbytes, uint64_t seed,
     hipLaunchKernelGGL(splitmix_fill, dim3(blocks), dim3(256), 0, (hipStream_t)stream, d_out,
                        nbytes, seed, word0);
     return hip_rc(hipGetLastError());
+}
+
+int noise_aead_dev_hkdf(int hash_id, const uint8_t *d_keys, uint32_t key_len,
+                        const uint8_t *d_data, uint32_t data_len, uint32_t n, uint8_t *d_out1,
+                        uint32_t out1_len, uint8_t *d_out2, uint32_t out2_len, void *stream)
+{
+    uint32_t hl;
+    switch (hash_id) {
+    case NOISE_HASH_BLAKE2s: case NOISE_HASH_SHA256: hl = 32; break;
+    case NOISE_HASH_BLAKE2b: case NOISE_HASH_SHA512: hl = 64; break;
+    default: return NOISE_ERROR_UNKNOWN_ID;
+    }
+    if (!n) return NOISE_ERROR_NONE;
+    if (!d_keys || !d_out1 || !d_out2 || (data_len && !d_data)) return NOISE_ERROR_INVALID_PARAM;
+    /* hashstate.c:496-497 */
+    if (out1_len > hl || out2_len > hl) return NOISE_ERROR_INVALID_LENGTH;
+    if (key_len == 0 || key_len > KDF_MAX_IN || data_len > KDF_MAX_IN)
+        return NOISE_ERROR_INVALID_LENGTH;
+    KdfArgs a;
+    a.hash_id = hash_id;
+    a.keys = d_keys;
+    a.data = data_len ? d_data : nullptr;
+    a.out1 = d_out1;
+    a.out2 = d_out2;
+    a.key_len = key_len;
+    a.data_len = data_len;
+    a.out1_len = out1_len;
+    a.out2_len = out2_len;
+    a.n = n;
+    hipLaunchKernelGGL(hkdf_batch, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, a);
+    return hip_rc(hipGetLastError());
+}
+
+int noise_aead_dev_split(int hash_id, const uint8_t *d_ck, uint32_t n, uint8_t *d_k1,
+                         uint8_t *d_k2, void *stream)
+{
+    const uint32_t hl = (hash_id == NOISE_HASH_BLAKE2b || hash_id == NOISE_HASH_SHA512) ? 64 : 32;
+    return noise_aead_dev_hkdf(hash_id, d_ck, hl, nullptr, 0, n, d_k1, 32, d_k2, 32, stream);
 }
 
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)

@@ -37,7 +37,11 @@ ERROR_INVALID_PARAM = NOISE_ID("E", 11)
 ERROR_INVALID_STATE = NOISE_ID("E", 12)
 ERROR_INVALID_NONCE = NOISE_ID("E", 13)
 MAX_PAYLOAD_LEN = 65535
-HASH_BLAKE2s = NOISE_ID("H", 1)
+HASH_BLAKE2s = NOISE_ID("H", 1)  # constants.h:43-46
+HASH_BLAKE2b = NOISE_ID("H", 2)
+HASH_SHA256 = NOISE_ID("H", 3)
+HASH_SHA512 = NOISE_ID("H", 4)
+HASH_LEN = {HASH_BLAKE2s: 32, HASH_BLAKE2b: 64, HASH_SHA256: 32, HASH_SHA512: 64}
 
 
 class NoiseBuffer(C.Structure):
@@ -123,6 +127,9 @@ def lib() -> C.CDLL:
         "noise_wire_seal": (i, [vp, vp, sz, P(sz), P(sz)]),
         "noise_wire_open": (i, [vp, vp, sz, P(sz), P(sz)]),
         "noise_wire_echo": (i, [vp, vp, vp, sz, P(sz), P(sz)]),
+        "noise_aead_dev_hkdf": (i, [i, vp, C.c_uint32, vp, C.c_uint32, C.c_uint32, vp,
+                                    C.c_uint32, vp, C.c_uint32, vp]),
+        "noise_aead_dev_split": (i, [i, vp, C.c_uint32, vp, vp, vp]),
         "noise_aead_dev_ctx_bytes": (sz, [i]),
         "noise_aead_dev_prepare": (i, [i, vp, C.c_uint32, vp, vp]),
         "noise_aead_dev_seal_uniform": (i, [i, P(NoiseAeadUniform), vp]),
@@ -349,6 +356,16 @@ def dev_ragged(open_: bool, cipher: int, *, ctx_base: int, recs: int, inp: int, 
                         n_records, lanes, flags, 0)
     f = lib().noise_aead_dev_open_ragged if open_ else lib().noise_aead_dev_seal_ragged
     return f(cipher, C.byref(j), stream or None)
+
+
+def dev_hkdf(hash_id: int, *, keys: int, key_len: int, data: int = 0, data_len: int = 0,
+             n: int, out1: int, out1_len: int, out2: int, out2_len: int, stream: int = 0) -> int:
+    return lib().noise_aead_dev_hkdf(hash_id, keys, key_len, data or None, data_len, n, out1,
+                                     out1_len, out2, out2_len, stream or None)
+
+
+def dev_split(hash_id: int, *, ck: int, n: int, k1: int, k2: int, stream: int = 0) -> int:
+    return lib().noise_aead_dev_split(hash_id, ck, n, k1, k2, stream or None)
 
 
 def dev_fill_splitmix(d_out: int, nbytes: int, seed: int, word0: int = 0, stream: int = 0) -> int:

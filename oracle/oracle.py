@@ -59,11 +59,28 @@ class Oracle:
         L.oracle_splitmix64.argtypes = [C.c_uint64]
         L.oracle_splitmix64.restype = C.c_uint64
         L.oracle_fill_splitmix.argtypes = [C.c_uint64, C.c_uint64, u8p, sz]
+        L.oracle_hash.argtypes = [C.c_int, u8p, sz, u8p]
+        L.oracle_hkdf.argtypes = [C.c_int, u8p, sz, u8p, sz, u8p, sz, u8p, sz]
         self.L = L
 
     @staticmethod
     def _p(b: bytearray):
         return C.addressof(_buf(b)) if len(b) else None
+
+    def hash(self, hash_id: int, data: bytes) -> bytes:
+        out = bytearray(64)
+        d = bytearray(data)
+        n = self.L.oracle_hash(hash_id, self._p(d), len(d), self._p(out))
+        assert n > 0
+        return bytes(out[:n])
+
+    def hkdf(self, hash_id: int, key: bytes, data: bytes, l1: int, l2: int):
+        """noise_hashstate_hkdf (hashstate.c:476-516)"""
+        o1, o2 = bytearray(max(l1, 1)), bytearray(max(l2, 1))
+        k, d = bytearray(key), bytearray(data)
+        assert self.L.oracle_hkdf(hash_id, self._p(k), len(k), self._p(d), len(d),
+                                  self._p(o1), l1, self._p(o2), l2) == 0
+        return bytes(o1[:l1]), bytes(o2[:l2])
 
     def encrypt(self, cipher: int, key: bytes, n: int, pt: bytes, ad: bytes = b"") -> bytes:
         data = bytearray(pt) + bytearray(16)

@@ -103,3 +103,29 @@ def test_splitmix_fill(oracle):
     assert oracle.splitmix64(0) == 0xE220A8397B1DCDAF
     b = oracle.fill(0, 16)
     assert int.from_bytes(b[:8], "little") == 0xE220A8397B1DCDAF
+
+
+def test_hash_oracle_standard_vectors(oracle):
+    """FIPS 180-4 / RFC 7693 'abc' vectors for the four Noise hashes
+    (noise_oracle_hash.c)."""
+    exp = {0x4803: "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad",
+           0x4804: "ddaf35a193617abacc417349ae20413112e6fa4e89a97ea20a9eeee64b55d39a"
+                   "2192992a274fc1a836ba3c23a3feebbd454d4423643ce80e2a9ac94fa54ca49f",
+           0x4801: "508c5e8c327c14e2e1a72ba34eeb452f37458b209ed63a294d999b4c86675982",
+           0x4802: "ba80a53f981c4d0d6a2797b69f12f6e94c212f14685ac4b74b12bb6fdbffa2d1"
+                   "7d87c5392aab792dc252d5de4533cc9518d38aa8dbf1925ab92386edd4009923"}
+    for hid, h in exp.items():
+        assert oracle.hash(hid, b"abc").hex() == h
+
+
+def test_hkdf_oracle_vs_reference_golden(oracle):
+    """tests/golden/hkdf.json: noise_hashstate_hkdf outputs of the reference
+    itself (gen_hkdf.py), split and mix_key shapes, all four hashes."""
+    import json
+    with open(os.path.join(os.path.dirname(__file__), "golden", "hkdf.json")) as f:
+        cases = json.load(f)["cases"]
+    assert len(cases) == 40
+    for c in cases:
+        o1, o2 = oracle.hkdf(c["hash_id"], bytes.fromhex(c["key"]), bytes.fromhex(c["data"]),
+                             len(c["out1"]) // 2, len(c["out2"]) // 2)
+        assert (o1.hex(), o2.hex()) == (c["out1"], c["out2"]), c
