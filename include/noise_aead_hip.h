@@ -257,6 +257,20 @@ int noise_aead_dev_hkdf(int hash_id, const uint8_t *d_keys, uint32_t key_len,
 int noise_aead_dev_split(int hash_id, const uint8_t *d_ck, uint32_t n, uint8_t *d_k1,
                          uint8_t *d_k2, void *stream);
 
+/* Handshake-payload AEAD for a batch of SymmetricStates (SURVEY.md §8f
+ * rank 3): noise_symmetricstate_encrypt_and_hash / decrypt_and_hash
+ * (symmetricstate.c:352-445) on n keyed states at once.  d_h holds the n
+ * handshake hashes (hash-length bytes each); the job's AD must be those
+ * hashes: job->ad == d_h and record i's ad_off = i * hash_len, ad_len =
+ * hash_len.  Encrypt seals record i with AD = h_i, then
+ * h_i = HASH(h_i || CT_i || tag_i).  Decrypt hashes CT_i || tag_i first,
+ * opens, and keeps the new h_i only where status[i] == 0 (the reference
+ * leaves h unchanged on a MAC failure, :425-443); job->status is required. */
+int noise_aead_dev_encrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
+                                    const NoiseAeadRagged *job, void *stream);
+int noise_aead_dev_decrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
+                                    const NoiseAeadRagged *job, void *stream);
+
 /* Default lanes per record the library picks for a batch of n records. */
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records);
 

@@ -347,6 +347,68 @@ int noise_aead_dev_split(int hash_id, const uint8_t *d_ck, uint32_t n, uint8_t *
     return noise_aead_dev_hkdf(hash_id, d_ck, hl, nullptr, 0, n, d_k1, 32, d_k2, 32, stream);
 }
 
+static uint32_t hash_len_of(int hash_id)
+{
+    switch (hash_id) {
+    case NOISE_HASH_BLAKE2s: case NOISE_HASH_SHA256: return 32;
+    case NOISE_HASH_BLAKE2b: case NOISE_HASH_SHA512: return 64;
+    }
+    return 0;
+}
+
+static int launch_mix_hash(int hash_id, uint32_t hl, const uint8_t *h_in, uint8_t *h_out,
+                           const NoiseAeadRagged *job, bool use_out, hipStream_t s)
+{
+    MixHashArgs m;
+    m.hash_id = hash_id;
+    m.hlen = hl;
+    m.n = job->n_records;
+    m.h_in = h_in;
+    m.h_out = h_out;
+    m.base = use_out ? job->out : job->in;
+    m.recs = (const RecDesc *)job->recs;
+    m.use_out_off = use_out;
+    hipLaunchKernelGGL(mix_hash_batch, dim3((job->n_records + 63) / 64), dim3(64), 0, s, m);
+    return hip_rc(hipGetLastError());
+}
+
+int noise_aead_dev_encrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
+                                    const NoiseAeadRagged *job, void *stream)
+{
+    const uint32_t hl = hash_len_of(hash_id);
+    if (!hl) return NOISE_ERROR_UNKNOWN_ID;
+    if (!d_h || !job || job->ad != d_h) return NOISE_ERROR_INVALID_PARAM;
+    if (job->n_records == 0) return NOISE_ERROR_NONE;
+    int rc = run_ragged(cipher_id, job, stream, false);
+    if (rc) return rc;
+    return launch_mix_hash(hash_id, hl, d_h, d_h, job, true, (hipStream_t)stream);
+}
+
+int noise_aead_dev_decrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
+                                    const NoiseAeadRagged *job, void *stream)
+{
+    const uint32_t hl = hash_len_of(hash_id);
+    if (!hl) return NOISE_ERROR_UNKNOWN_ID;
+    if (!d_h || !job || job->ad != d_h || !job->status) return NOISE_ERROR_INVALID_PARAM;
+    if (job->n_records == 0) return NOISE_ERROR_NONE;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t bytes = (size_t)job->n_records * hl;
+    uint8_t *h_new = nullptr;
+    if (hipMallocAsync((void **)&h_new, bytes, s) != hipSuccess) return NOISE_ERROR_NO_MEMORY;
+    /* hash the ciphertext before the (in-place) decryption overwrites it */
+    int rc = launch_mix_hash(hash_id, hl, d_h, h_new, job, false, s);
+    if (!rc) rc = run_ragged(cipher_id, job, stream, true);
+    if (!rc) {
+        const uint32_t total = job->n_records * hl;
+        hipLaunchKernelGGL(commit_hash, dim3((total + 255) / 256), dim3(256), 0, s, d_h,
+                           (const uint8_t *)h_new, (const uint8_t *)job->status, hl,
+                           job->n_records);
+        rc = hip_rc(hipGetLastError());
+    }
+    (void)hipFreeAsync(h_new, s);
+    return rc;
+}
+
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)
 {
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) return auto_lanes(n_records);

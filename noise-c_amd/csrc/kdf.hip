@@ -311,4 +311,44 @@ __global__ __launch_bounds__(64) void hkdf_batch(KdfArgs a)
     for (int j = 0; j < 64; ++j) tk[j] = 0; /* hashstate.c:512-513 cleans its temporaries */
 }
 
+/* ------------------------------------------------ handshake-payload MixHash
+ *
+ * noise_symmetricstate_{encrypt,decrypt}_and_hash (symmetricstate.c
+ * :352-445) for a batch of SymmetricStates: after (before, for decrypt) the
+ * AEAD of record i under AD = h_i, h_i = HASH(h_i || ciphertext_i || tag_i)
+ * (noise_symmetricstate_mix_hash, :244-258).  One lane per record. */
+struct MixHashArgs {
+    int hash_id;
+    uint32_t hlen, n;
+    const uint8_t *h_in;
+    uint8_t *h_out;
+    const uint8_t *base;   /* the job's `out` (encrypt) or `in` (decrypt) */
+    const RecDesc *recs;
+    int use_out_off;
+};
+
+__global__ __launch_bounds__(64) void mix_hash_batch(MixHashArgs a)
+{
+    const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+    if (i >= a.n) return;
+    const RecDesc d = a.recs[i];
+    Hasher H;
+    H.init(a.hash_id);
+    uint8_t h[64];
+    for (uint32_t j = 0; j < a.hlen; ++j) h[j] = a.h_in[(size_t)i * a.hlen + j];
+    H.update(h, a.hlen);
+    H.update(a.base + (a.use_out_off ? d.out_off : d.in_off), d.len + 16);
+    H.final(h);
+    for (uint32_t j = 0; j < a.hlen; ++j) a.h_out[(size_t)i * a.hlen + j] = h[j];
+}
+
+/* decrypt_and_hash keeps the new hash only when the tag verified (:436-443) */
+__global__ __launch_bounds__(256) void commit_hash(uint8_t *h, const uint8_t *h_new,
+                                                   const uint8_t *status, uint32_t hlen, uint32_t n)
+{
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= n * hlen) return;
+    if (status[t / hlen] == 0) h[t] = h_new[t];
+}
+
 } // namespace na

@@ -130,6 +130,8 @@ def lib() -> C.CDLL:
         "noise_aead_dev_hkdf": (i, [i, vp, C.c_uint32, vp, C.c_uint32, C.c_uint32, vp,
                                     C.c_uint32, vp, C.c_uint32, vp]),
         "noise_aead_dev_split": (i, [i, vp, C.c_uint32, vp, vp, vp]),
+        "noise_aead_dev_encrypt_and_hash": (i, [i, i, vp, P(NoiseAeadRagged), vp]),
+        "noise_aead_dev_decrypt_and_hash": (i, [i, i, vp, P(NoiseAeadRagged), vp]),
         "noise_aead_dev_ctx_bytes": (sz, [i]),
         "noise_aead_dev_prepare": (i, [i, vp, C.c_uint32, vp, vp]),
         "noise_aead_dev_seal_uniform": (i, [i, P(NoiseAeadUniform), vp]),
@@ -362,6 +364,18 @@ def dev_hkdf(hash_id: int, *, keys: int, key_len: int, data: int = 0, data_len: 
              n: int, out1: int, out1_len: int, out2: int, out2_len: int, stream: int = 0) -> int:
     return lib().noise_aead_dev_hkdf(hash_id, keys, key_len, data or None, data_len, n, out1,
                                      out1_len, out2, out2_len, stream or None)
+
+
+def dev_and_hash(open_: bool, cipher: int, hash_id: int, *, ctx_base: int, h: int, recs: int,
+                 inp: int, out: int, n_records: int, status: int = 0, flags: int = 0,
+                 stream: int = 0) -> int:
+    """noise_aead_dev_{en,de}crypt_and_hash: AD = the hashes at h; record
+    ctx_off values are offsets from ctx_base (as dev_ragged)."""
+    j = NoiseAeadRagged(ctx_base or None, recs, inp, out, h, status or None, n_records, 0,
+                        flags, 0)
+    f = (lib().noise_aead_dev_decrypt_and_hash if open_ else
+         lib().noise_aead_dev_encrypt_and_hash)
+    return f(cipher, hash_id, h, C.byref(j), stream or None)
 
 
 def dev_split(hash_id: int, *, ck: int, n: int, k1: int, k2: int, stream: int = 0) -> int:

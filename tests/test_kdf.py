@@ -117,3 +117,74 @@ def test_split_keys_drive_transport(aead, gpu, oracle, cipher):
     for i in range(n):
         key1, _ = oracle.hkdf(0x4801, bytes(ck[i]), b"", 32, 32)
         assert bytes(ct[i, :L + 16]) == oracle.encrypt(cipher, key1, 0, bytes(pt[i, :L])), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cipher,hid", [(0x4301, 0x4801), (0x4302, 0x4803), (0x4301, 0x4804),
+                                        (0x4302, 0x4802)])
+def test_encrypt_and_hash_batch(aead, gpu, oracle, cipher, hid):
+    """noise_symmetricstate_{encrypt,decrypt}_and_hash (symmetricstate.c
+    :352-445) for 300 states at once: AD = h_i; h_i <- HASH(h_i || CT || tag);
+    a record whose tag fails keeps its old h and its ciphertext."""
+    import torch
+    rng = np.random.default_rng(cipher + hid)
+    n, hl = 300, HLEN[hid]
+    keys = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    d_keys = torch.from_numpy(keys.reshape(-1).copy()).cuda()
+    cb = aead.dev_ctx_bytes(cipher)
+    ctx = torch.empty(n * cb, dtype=torch.uint8, device="cuda")
+    sp = torch.cuda.current_stream().cuda_stream
+    assert aead.dev_prepare(cipher, d_keys.data_ptr(), n, ctx.data_ptr(), sp) == 0
+    h0 = rng.integers(0, 256, (n, hl), dtype=np.uint8)
+    lens = rng.integers(0, 1500, n)
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum(lens + 16 + 7)[:-1]
+    total = int(offs[-1] + lens[-1] + 16 + 64)
+    pt = rng.integers(0, 256, total, dtype=np.uint8)
+    nonces = rng.integers(0, 2**40, n).astype(np.uint64)
+    dt = [("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "<u8"),
+          ("ad_off", "<u8"), ("len", "<u4"), ("ad_len", "<u4")]
+    recs = np.zeros(n, dtype=dt)
+    recs["in_off"] = recs["out_off"] = offs
+    recs["nonce"] = nonces
+    recs["ctx_off"] = np.arange(n, dtype=np.uint64) * cb
+    recs["ad_off"] = np.arange(n, dtype=np.uint64) * hl
+    recs["len"] = lens
+    recs["ad_len"] = hl
+    d_recs = torch.from_numpy(recs.view(np.uint8).copy()).cuda()
+    d_buf = torch.from_numpy(pt.copy()).cuda()
+    d_h = torch.from_numpy(h0.reshape(-1).copy()).cuda()
+    kw = dict(ctx_base=ctx.data_ptr(), h=d_h.data_ptr(), recs=d_recs.data_ptr(), inp=d_buf.data_ptr(),
+              out=d_buf.data_ptr(), n_records=n, stream=sp)
+    # job->ad must be the hashes
+    assert aead.dev_and_hash(False, cipher, hid, **kw) == 0
+    torch.cuda.synchronize()
+    ct = d_buf.cpu().numpy()
+    h1 = d_h.cpu().numpy().reshape(n, hl)
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        exp = oracle.encrypt(cipher, bytes(keys[i]), int(nonces[i]), bytes(pt[o:o + L]),
+                             bytes(h0[i]))
+        assert bytes(ct[o:o + L + 16]) == exp, i
+        assert bytes(h1[i]) == oracle.hash(hid, bytes(h0[i]) + exp), i
+    # the receiving side: same h0, tampered records fail and keep h0
+    bad = np.arange(n) % 23 == 4
+    tampered = ct.copy()
+    for i in np.nonzero(bad)[0]:
+        tampered[int(offs[i]) + int(lens[i]) + 3] ^= 1
+    d_buf = torch.from_numpy(tampered.copy()).cuda()
+    d_h = torch.from_numpy(h0.reshape(-1).copy()).cuda()
+    d_st = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    kw.update(h=d_h.data_ptr(), inp=d_buf.data_ptr(), out=d_buf.data_ptr())
+    assert aead.dev_and_hash(True, cipher, hid, status=d_st.data_ptr(), **kw) == 0
+    torch.cuda.synchronize()
+    st, back, h2 = d_st.cpu().numpy(), d_buf.cpu().numpy(), d_h.cpu().numpy().reshape(n, hl)
+    assert np.array_equal(st != 0, bad)
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        if bad[i]:
+            assert bytes(h2[i]) == bytes(h0[i]) and np.array_equal(back[o:o + L + 16],
+                                                                   tampered[o:o + L + 16]), i
+        else:
+            assert np.array_equal(back[o:o + L], pt[o:o + L]), i
+            assert bytes(h2[i]) == oracle.hash(hid, bytes(h0[i]) + bytes(ct[o:o + L + 16])), i
