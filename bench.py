@@ -216,6 +216,8 @@ def main():
     ap.add_argument("--no-xfer", action="store_true",
                     help="skip the N>1 scatter/seal/gather leg (RCCL, SURVEY.md 8e)")
     ap.add_argument("--xfer-reps", type=int, default=5)
+    ap.add_argument("--c5-streams", type=int, default=2, choices=(1, 2),
+                    help="C5: 2 = the AES-GCM and ChaChaPoly halves on two streams, concurrently")
     args = ap.parse_args()
 
     import torch
@@ -502,19 +504,36 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                            bytes=int(lay["lens"][idx].sum()), states=len(states)))
     torch.cuda.synchronize(dev)
 
-    def launch(g, open_):
+    def launch(g, open_, stream=sp):
         return A.dev_ragged(open_, g["cipher"], ctx_base=g["ctx"].data_ptr(),
                             recs=g["recs"].data_ptr(), inp=(ct if open_ else pt).data_ptr(),
                             out=(back if open_ else ct).data_ptr(), n_records=g["n"],
                             status=g["st"].data_ptr() if open_ else 0, lanes=args.lanes,
-                            flags=A.FLAG_FAST, stream=sp)
+                            flags=A.FLAG_FAST, stream=stream)
+
+    # Two streams: the LDS-bound AES-GCM kernel and the VALU-bound ChaChaPoly
+    # kernel share the CUs instead of running back to back; the open phase
+    # waits for both seals (fork/join by events, no host sync).
+    main_s = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev) if args.c5_streams == 2 and len(groups) == 2 else None
+    fork = [torch.cuda.Event() for _ in range(2)]
+    join = [torch.cuda.Event() for _ in range(2)]
 
     def step():
         for open_ in (False, True):
-            for g in groups:
-                rc = launch(g, open_)
-                if rc:
-                    raise RuntimeError(f"launch failed {rc:#x}")
+            if side is None:
+                for g in groups:
+                    rc = launch(g, open_)
+                    if rc:
+                        raise RuntimeError(f"launch failed {rc:#x}")
+                continue
+            fork[open_].record(main_s)
+            side.wait_event(fork[open_])
+            rc = launch(groups[1], open_, side.cuda_stream) or launch(groups[0], open_)
+            if rc:
+                raise RuntimeError(f"launch failed {rc:#x}")
+            join[open_].record(side)
+            main_s.wait_event(join[open_])
 
     for _ in range(args.warmup):
         step()
@@ -568,6 +587,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
         "data": "synthetic (SplitMix64 lengths, plaintext and keys, SURVEY.md 8d C5), resident in HBM",
         "config": {"workload": cfg["workload"], "config": "c5", "records_per_gpu": R,
                    "states_per_gpu": S, "payload_bytes_per_step": int(2 * payload * world),
+                   "streams": 2 if side is not None else 1,
                    "parallelism": f"states x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
