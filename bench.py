@@ -119,8 +119,31 @@ def stride(n: int) -> int:
     return (n + IN_ALIGN - 1) // IN_ALIGN * IN_ALIGN
 
 
+def host_cpu():
+    """CPU model and the CPUs this process may use (SURVEY.md 8d asks for both)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+
+
 def cpu_baseline(cfg, budget_cpu_s: float = 12.0):
     """Reference noise-c (oracle/_ref/ref_bench), bounded sample."""
+    r = _cpu_baseline(cfg, budget_cpu_s)
+    return None if r is None else {**r, **host_cpu()}
+
+
+def _cpu_baseline(cfg, budget_cpu_s):
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
     kind = "reference"
     if not os.path.exists(ref):
