@@ -42,12 +42,23 @@ hipError_t ensure_aes_tables(hipStream_t stream)
 }
 
 /* Lanes per record for ChaChaPoly: 4 (the fastest split at 64 Ki and 1 Mi
-   records, profiles/r01_sweep_*), 8 when the batch is too small to give every
-   SIMD four waves that way. */
-int auto_lanes(uint32_t n_records)
+   records, profiles/r01_sweep_*); a batch too small to give every SIMD four
+   waves that way gets wider groups, up to one wave per record — that is the
+   single-call latency path, where a long record's blocks would otherwise run
+   serially on a few lanes.  No wider than the longest record needs (two
+   ChaCha blocks per lane); max_len = 0 when unknown (device descriptors). */
+int auto_lanes(uint32_t n_records, uint32_t max_len)
 {
-    const uint64_t target = 256ull * 16 * 64;
-    return (uint64_t)n_records * 4 < target ? 8 : 4;
+    const uint64_t target = 256ull * 16 * 64; /* 4 waves on each of 1024 SIMDs */
+    int k = 4;
+    while (k < 64 && (uint64_t)n_records * k < target) k <<= 1;
+    if (max_len) {
+        const uint32_t blocks = (max_len + 63) / 64 + 1;
+        int need = 4;
+        while (need < 64 && (uint32_t)need * 2 < blocks) need <<= 1;
+        if (k > need) k = need;
+    }
+    return k;
 }
 
 template <typename Args>
@@ -82,6 +93,9 @@ KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey)
     case 8:
         if (FAST) return chacha_staged_fn<8>(open, ukey);
         return open ? chachapoly_open_uniform<8, FAST> : chachapoly_seal_uniform<8, FAST>;
+    case 16: return open ? chachapoly_open_uniform<16, FAST> : chachapoly_seal_uniform<16, FAST>;
+    case 32: return open ? chachapoly_open_uniform<32, FAST> : chachapoly_seal_uniform<32, FAST>;
+    case 64: return open ? chachapoly_open_uniform<64, FAST> : chachapoly_seal_uniform<64, FAST>;
     }
     return nullptr;
 }
@@ -100,6 +114,9 @@ KernelFn<RaggedArgs> chacha_ragged_fn_t(int k, bool open)
     case 2: return open ? chachapoly_open_ragged<2, FAST> : chachapoly_seal_ragged<2, FAST>;
     case 4: return open ? chachapoly_open_ragged<4, FAST> : chachapoly_seal_ragged<4, FAST>;
     case 8: return open ? chachapoly_open_ragged<8, FAST> : chachapoly_seal_ragged<8, FAST>;
+    case 16: return open ? chachapoly_open_ragged<16, FAST> : chachapoly_seal_ragged<16, FAST>;
+    case 32: return open ? chachapoly_open_ragged<32, FAST> : chachapoly_seal_ragged<32, FAST>;
+    case 64: return open ? chachapoly_open_ragged<64, FAST> : chachapoly_seal_ragged<64, FAST>;
     }
     return nullptr;
 }
@@ -158,7 +175,7 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     hipStream_t s = (hipStream_t)stream;
     const UniformArgs a = to_args(job);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
-        int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records);
+        int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
         const bool ukey = k >= 4 && job->recs_per_state % (64u / (uint32_t)k) == 0;
         KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open), ukey);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
@@ -196,7 +213,7 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
     a.status = job->status;
     a.n_records = job->n_records;
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
-        int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records);
+        int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
         KernelFn<RaggedArgs> fn =
             chacha_ragged_fn(k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
@@ -209,6 +226,13 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
         /* LDS-staged kernel: 1024-thread workgroups over 256-record windows;
            a batch too small to give every CU one of those uses 256-thread
            workgroups over 64-record windows instead (4x the workgroups) */
+        if (job->lanes_per_record == 0 && job->n_records <= GCM_WIDE_MAX_RECORDS) {
+            /* small batch: a workgroup per record (latency, not throughput);
+               lanes_per_record = 4 keeps the windowed 4-lane kernels */
+            hipLaunchKernelGGL(open ? gcm_wide<true> : gcm_wide<false>, dim3(job->n_records),
+                               dim3(256), 0, s, a);
+            return hip_rc(hipGetLastError());
+        }
         const bool fast = (job->flags & NOISE_AEAD_FLAG_FAST) != 0;
         const bool big = job->n_records >= 256u * GCM_WG_RECS;
         const uint32_t per = big ? GCM_WG_RECS : GCM_WG_RECS / 4;
@@ -411,9 +435,15 @@ int noise_aead_dev_decrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
 
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)
 {
-    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) return auto_lanes(n_records);
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) return auto_lanes(n_records, 0);
     if (cipher_id == NOISE_CIPHER_AESGCM) return GCM_LANES;
     return 0;
+}
+
+/* host_internal.h: the host paths know their records' lengths */
+__attribute__((visibility("hidden"))) uint32_t na_chacha_lanes(uint32_t n_records, uint32_t max_len)
+{
+    return (uint32_t)auto_lanes(n_records, max_len ? max_len : 1);
 }
 
 } // extern "C"

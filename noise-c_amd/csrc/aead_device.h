@@ -181,6 +181,7 @@ NA_DEV Fe fe_group_sum(Fe h)
 {
 #pragma unroll
     for (int off = 1; off < G; off <<= 1) {
+        if (off == 32) h = fe_carry(h); /* 32 summed limbs reach 2^31 */
         h.l0 += (uint32_t)__shfl_xor((int)h.l0, off, 64);
         h.l1 += (uint32_t)__shfl_xor((int)h.l1, off, 64);
         h.l2 += (uint32_t)__shfl_xor((int)h.l2, off, 64);

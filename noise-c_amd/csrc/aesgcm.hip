@@ -797,5 +797,109 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
     if (OPEN && l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
+/* ------------------------------------------ wide (small batches, latency)
+ *
+ * One record per 256-thread workgroup, for batches too small to fill the
+ * chip four lanes per record (the single-call path of noise_cipherstate_*,
+ * short wire buffers).  The record's CTR blocks are spread over all 256
+ * threads; GHASH is gcm_record's 4-lane Horner (H^4 steps, scale by
+ * H^(4-l), XOR-reduce) run by lanes 0..3 with the H^4 table in LDS.  Seal:
+ * CTR, then GHASH over the CT just written.  Open: GHASH and tag check
+ * first, CTR only when the tag verified (cipher-aesgcm.c:184-186).
+ */
+constexpr uint32_t GCM_WIDE_MAX_RECORDS = 4096; /* aead_api.hip run_ragged */
+
+template <bool OPEN>
+__global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
+{
+    constexpr int K = GCM_LANES;
+    __shared__ uint32_t te[256], sb[256];
+    __shared__ uint4 h4[GHASH_TAB_ENTRIES];
+    __shared__ uint32_t verdict;
+    const uint32_t rec = blockIdx.x, t = threadIdx.x;
+    const RecDesc d = a.recs[rec];
+    const AesCtx *ctx = (const AesCtx *)(a.keys + d.ctx_off);
+    const uint8_t *src = a.in + d.in_off;
+    uint8_t *dst = a.out + d.out_off;
+    const uint32_t len = d.len, M = (len + 15) / 16;
+    for (uint32_t i = t; i < 256; i += 256) {
+        te[i] = g_te0[i];
+        sb[i] = g_sbox[i];
+    }
+    for (uint32_t i = t; i < (uint32_t)GHASH_TAB_ENTRIES; i += 256)
+        h4[i] = ((const uint4 *)ctx->tab[K - 1])[i];
+    __syncthreads();
+    const uint32_t *rk = ctx->rk;
+
+    if (!OPEN) {
+        for (uint32_t b = t; b < M; b += 256) {
+            const uint32_t nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
+            uint32_t x[4], ks[4];
+            load16(src + 16 * b, nb, x);
+            aes_ctr_block(rk, te, sb, d.nonce, 2 + b, ks);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+            store16(dst + 16 * b, nb, x);
+        }
+        __threadfence(); /* the GHASH lanes read this CT back */
+        __syncthreads();
+        __threadfence();
+    }
+    if (t < (uint32_t)K) {
+        const int l = (int)t;
+        const uint8_t *ct = OPEN ? src : dst;
+        const uint32_t A = (d.ad_len + 15) / 16, n = A + M + 1;
+        const uint32_t c0 = ((uint32_t)l + n) % K;
+        uint32_t acc[4] = {0, 0, 0, 0};
+        for (uint32_t i = c0; i < n; i += K) {
+            if (i != c0) gh_mul_lds(acc, h4);
+            uint32_t x[4];
+            if (i < A) {
+                const uint32_t rem = d.ad_len - 16 * i;
+                load16(a.ad + d.ad_off + 16 * i, rem >= 16 ? 16u : rem, x);
+            } else if (i < A + M) {
+                const uint32_t b = i - A, rem = len - 16 * b;
+                load16(ct + 16 * b, rem >= 16 ? 16u : rem, x);
+            } else {
+                const uint64_t ab = (uint64_t)d.ad_len * 8, cb = (uint64_t)len * 8;
+                x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
+                x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
+            }
+            acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
+        }
+        gh_mul(acc, (const uint4 *)ctx->tab[K - 1 - l]);
+#pragma unroll
+        for (int off = 1; off < K; off <<= 1)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+        uint32_t ej[4];
+        aes_ctr_block(rk, te, sb, d.nonce, 1u, ej);
+        const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
+        if (!OPEN) {
+            if (l == K - 1) store16(dst + len, 16, tag);
+        } else if (l == 0) {
+            uint32_t got[4];
+            load16(src + len, 16, got);
+            const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) |
+                             (tag[3] ^ got[3])) == 0;
+            verdict = ok;
+            if (a.status) a.status[rec] = ok ? 0 : 1;
+        }
+    }
+    if (OPEN) {
+        __syncthreads();
+        if (!verdict) return; /* nothing decrypted */
+        for (uint32_t b = t; b < M; b += 256) {
+            const uint32_t nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
+            uint32_t x[4], ks[4];
+            load16(src + 16 * b, nb, x);
+            aes_ctr_block(rk, te, sb, d.nonce, 2 + b, ks);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+            store16(dst + 16 * b, nb, x);
+        }
+    }
+}
+
 } // namespace na
 

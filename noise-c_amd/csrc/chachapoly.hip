@@ -206,11 +206,31 @@ NA_DEV void poly_key_bcast(const uint32_t x[16], int src_lane, Fe &r, uint32_t s
     s[0] = kw[4]; s[1] = kw[5]; s[2] = kw[6]; s[3] = kw[7];
 }
 
+/* r^e for 1 <= e < 2^9, square-and-multiply (the wide groups' powers). */
+NA_DEV Fe fe_pow(Fe b, uint32_t e)
+{
+    Fe acc = Fe{1, 0, 0, 0, 0};
+    for (;;) {
+        if (e & 1) acc = fe_mul(acc, mk_mul(b));
+        e >>= 1;
+        if (!e) break;
+        b = fe_mul(b, mk_mul(b));
+    }
+    return acc;
+}
+
 /* The inter-unit jump r^(4K-3) and the final scale of lane k. */
 template <int K>
 NA_DEV void poly_powers(const Fe &r, int k, uint32_t q, Mul &mjump, Mul &mfinal)
 {
     const Mul mr = mk_mul(r);
+    if constexpr (K >= 16) {
+        /* wide groups (small batches of long records): lane k < K-1 is
+           scaled by r^(4(K-1-k)+q-2), as below, by direct powers */
+        mjump = mk_mul(fe_pow(r, 4 * K - 3));
+        mfinal = (k == K - 1) ? mr : mk_mul(fe_pow(r, 4u * (uint32_t)(K - 1 - k) + q - 2));
+        return;
+    }
     const Fe r2 = fe_mul(r, mr);
     const Mul m2 = mk_mul(r2);
     const Fe r4 = fe_mul(r2, m2);
@@ -989,7 +1009,7 @@ NA_DEV bool open_ct(const RecView &rv, int k)
 #define NA_UNIFORM_OCC __attribute__((amdgpu_waves_per_eu(4)))
 #endif
 
-/* lanes per record: 1 or 2 -> contiguous runs, 4 or 8 -> interleaved units */
+/* lanes per record: 1 or 2 -> contiguous runs, 4 .. 64 -> interleaved units */
 template <int K, bool FAST>
 NA_DEV void seal_any(const RecView &rv, int k)
 {

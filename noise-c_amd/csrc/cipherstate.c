@@ -106,9 +106,11 @@ Staging *na_stage_get(size_t bytes)
         if (s->h) (void)hipHostFree(s->h);
         if (s->d) (void)hipFree(s->d);
         s->h = NULL;
+        s->hd = NULL;
         s->d = NULL;
         s->cap = 0;
         if (hipHostMalloc((void **)&s->h, cap, hipHostMallocDefault) != hipSuccess) return NULL;
+        if (hipHostGetDevicePointer((void **)&s->hd, s->h, 0) != hipSuccess) return NULL;
         if (hipMalloc((void **)&s->d, cap) != hipSuccess) return NULL;
         s->cap = cap;
     }
@@ -176,6 +178,7 @@ typedef struct {
     size_t j0, j1;              /* jobs [j0, j1) */
     size_t recs_off, status_off, payload_off, end;
     uint32_t n_chacha, n_aes;
+    uint32_t chacha_max_len;    /* longest ChaChaPoly record (lane choice) */
 } Chunk;
 
 static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -244,6 +247,7 @@ static size_t plan_chunk(Job *jobs, Chunk *c, size_t at)
     size_t p = c->payload_off;
     uint32_t desc = 0;
     c->n_chacha = c->n_aes = 0;
+    c->chacha_max_len = 0;
     /* ChaCha20-Poly1305 descriptors first, then AES-GCM: one ragged launch each */
     for (int pass = 0; pass < 2; ++pass) {
         int want = pass == 0 ? NOISE_CIPHER_CHACHAPOLY : NOISE_CIPHER_AESGCM;
@@ -255,8 +259,12 @@ static size_t plan_chunk(Job *jobs, Chunk *c, size_t at)
             p += align16(j->ad_len);
             j->off = p;
             p += slot_bytes(j->len);
-            if (pass == 0) ++c->n_chacha;
-            else ++c->n_aes;
+            if (pass == 0) {
+                ++c->n_chacha;
+                if (j->len > c->chacha_max_len) c->chacha_max_len = (uint32_t)j->len;
+            } else {
+                ++c->n_aes;
+            }
         }
     }
     c->end = p;
@@ -279,27 +287,43 @@ static void fill_descriptors(Job *jobs, const Chunk *c, uint8_t *h)
     }
 }
 
-/* Chunk ci: H2D on the copy-in stream, then (on the main stream, after it)
-   the ragged kernels and the D2H of statuses + payload. */
-static int launch_chunk(Staging *sg, const Chunk *c, int ci, int open)
+/* Batches of at most this many staged bytes, in one chunk, skip both DMA
+   copies: the kernels read and write the pinned staging area over PCIe
+   (zero-copy).  For a single small record that removes two copy-engine round
+   trips from the call's latency.  NOISE_AEAD_ZERO_COPY_MAX overrides (0 = off). */
+static size_t zero_copy_max(void)
 {
-    if (hipMemcpyAsync(sg->d + c->recs_off, sg->h + c->recs_off, c->end - c->recs_off,
-                       hipMemcpyHostToDevice, sg->stream_in) != hipSuccess ||
-        hipEventRecord(sg->ev_in[ci], sg->stream_in) != hipSuccess ||
-        hipStreamWaitEvent(sg->stream, sg->ev_in[ci], 0) != hipSuccess)
+    static size_t v = (size_t)-1;
+    if (v == (size_t)-1) {
+        const char *e = getenv("NOISE_AEAD_ZERO_COPY_MAX");
+        v = e ? (size_t)strtoull(e, NULL, 10) : ZERO_COPY_DEFAULT;
+    }
+    return v;
+}
+
+/* Chunk ci: H2D on the copy-in stream, then (on the main stream, after it)
+   the ragged kernels and the D2H of statuses + payload — or, zero-copy, the
+   kernels alone on the staging bytes in host memory. */
+static int launch_chunk(Staging *sg, const Chunk *c, int ci, int open, int zc)
+{
+    uint8_t *base = zc ? sg->hd : sg->d;
+    if (!zc && (hipMemcpyAsync(sg->d + c->recs_off, sg->h + c->recs_off, c->end - c->recs_off,
+                               hipMemcpyHostToDevice, sg->stream_in) != hipSuccess ||
+                hipEventRecord(sg->ev_in[ci], sg->stream_in) != hipSuccess ||
+                hipStreamWaitEvent(sg->stream, sg->ev_in[ci], 0) != hipSuccess))
         return NOISE_ERROR_SYSTEM;
     for (int k = 0; k < 2; ++k) {
         uint32_t first = k == 0 ? 0 : c->n_chacha, count = k == 0 ? c->n_chacha : c->n_aes;
         if (!count) continue;
         NoiseAeadRagged job;
         job.ctx_base = NULL;
-        job.recs = (const NoiseAeadRecord *)(sg->d + c->recs_off) + first;
-        job.in = sg->d;
-        job.out = sg->d;
-        job.ad = sg->d;
-        job.status = sg->d + c->status_off + first;
+        job.recs = (const NoiseAeadRecord *)(base + c->recs_off) + first;
+        job.in = base;
+        job.out = base;
+        job.ad = base;
+        job.status = base + c->status_off + first;
         job.n_records = count;
-        job.lanes_per_record = 0;
+        job.lanes_per_record = k == 0 ? na_chacha_lanes(count, c->chacha_max_len) : 0;
         job.flags = NOISE_AEAD_FLAG_FAST;
         job.reserved_ = 0;
         int cid = k == 0 ? NOISE_CIPHER_CHACHAPOLY : NOISE_CIPHER_AESGCM;
@@ -307,8 +331,9 @@ static int launch_chunk(Staging *sg, const Chunk *c, int ci, int open)
                       : noise_aead_dev_seal_ragged(cid, &job, sg->stream);
         if (rc) return rc;
     }
-    if (hipMemcpyAsync(sg->h + c->status_off, sg->d + c->status_off, c->end - c->status_off,
-                       hipMemcpyDeviceToHost, sg->stream) != hipSuccess ||
+    if ((!zc && hipMemcpyAsync(sg->h + c->status_off, sg->d + c->status_off,
+                               c->end - c->status_off, hipMemcpyDeviceToHost,
+                               sg->stream) != hipSuccess) ||
         hipEventRecord(sg->ev_out[ci], sg->stream) != hipSuccess)
         return NOISE_ERROR_SYSTEM;
     return NOISE_ERROR_NONE;
@@ -408,7 +433,11 @@ static int run_jobs(Job *jobs, size_t n, int open, decide_fn decide, void *u)
         CopyArg a = {jobs + ch->j0, sg->h, open, 0};
         host_pool_for(ch->j1 - ch->j0, copy_grain(ch, ch->j1 - ch->j0), pack_range, &a);
         if (tr) t_pack += na_now_ms() - t0;
-        rc = launch_chunk(sg, ch, c, open);
+        /* AES-GCM's GHASH lanes read the CT serially: over PCIe that only
+           pays for the smallest records (profiles/r01_latency.jsonl) */
+        const size_t zmax = zero_copy_max();
+        rc = launch_chunk(sg, ch, c, open,
+                          nc == 1 && at <= (ch->n_aes && zmax > ZERO_COPY_AES ? ZERO_COPY_AES : zmax));
         if (rc) break;
         ++launched;
         if (c > 0) {

@@ -52,6 +52,8 @@ typedef struct {
 
 #define MAX_CHUNKS 64
 #define CHUNK_MIN ((size_t)4 << 20)
+#define ZERO_COPY_DEFAULT ((size_t)128 << 10) /* cipherstate.c zero_copy_max */
+#define ZERO_COPY_AES ((size_t)2 << 10)       /* ... with AES-GCM records in the batch */
 
 typedef struct {
     int device;
@@ -60,6 +62,7 @@ typedef struct {
     hipStream_t stream_out; /* wire path: host-gated kernels + D2H */
     hipEvent_t ev_in[MAX_CHUNKS], ev_out[MAX_CHUNKS], ev_done[MAX_CHUNKS];
     uint8_t *h;        /* pinned host */
+    uint8_t *hd;       /* the same pinned bytes as the device addresses them */
     uint8_t *d;        /* device */
     size_t cap;
 } Staging;
@@ -68,6 +71,8 @@ NA_HIDDEN Staging *na_stage_get(size_t bytes);
 NA_HIDDEN int na_ensure_ctx(HipCipherState *st, Staging *sg);
 NA_HIDDEN int na_is_ours(const NoiseCipherState *st);
 NA_HIDDEN void na_clean(void *p, size_t n);
+/* ChaChaPoly lanes per record for n records of at most max_len bytes (aead_api.hip) */
+NA_HIDDEN uint32_t na_chacha_lanes(uint32_t n_records, uint32_t max_len);
 /* memcpy with non-temporal (streaming) stores: staging copies are written
    once and read back by DMA or by another pass much later, so skipping the
    read-for-ownership of every destination line halves their write traffic */

@@ -103,6 +103,7 @@ typedef struct {
     size_t w0, w1;             /* wire bytes [w0, w1) */
     size_t prefix;             /* open/echo: frames of the chunk that verified, in order */
     int failed;                /* a frame of this chunk failed its MAC */
+    uint32_t max_len;          /* longest frame (ChaChaPoly lane choice) */
 } WChunk;
 
 typedef struct {
@@ -140,7 +141,7 @@ static void fill_desc(NoiseAeadRecord *d, const Frame *f, uint64_t nonce, const 
 
 static int launch_ragged(int open, const HipCipherState *st, const uint8_t *d_base,
                          const NoiseAeadRecord *d_recs, uint8_t *d_status, size_t n,
-                         hipStream_t s)
+                         uint32_t max_len, hipStream_t s)
 {
     NoiseAeadRagged job;
     job.ctx_base = NULL;
@@ -150,7 +151,8 @@ static int launch_ragged(int open, const HipCipherState *st, const uint8_t *d_ba
     job.ad = d_base;
     job.status = d_status;
     job.n_records = (uint32_t)n;
-    job.lanes_per_record = 0;
+    job.lanes_per_record = st->parent.cipher_id == NOISE_CIPHER_CHACHAPOLY
+                               ? na_chacha_lanes((uint32_t)n, max_len) : 0;
     job.flags = 0; /* frames sit at 2-byte offsets: the any-alignment kernels */
     job.reserved_ = 0;
     return open ? noise_aead_dev_open_ragged(st->parent.cipher_id, &job, s)
@@ -230,6 +232,9 @@ static int wire_run(int mode, NoiseCipherState *sa, NoiseCipherState *sb, uint8_
             meta = (c->status_off + n + 63) & ~(size_t)63;
             c->prefix = 0;
             c->failed = 0;
+            c->max_len = 0;
+            for (size_t f = c->f0; f < c->f1; ++f)
+                if (fr[f].len > c->max_len) c->max_len = fr[f].len;
             f0 = k + 1;
         }
     }
@@ -269,7 +274,7 @@ static int wire_run(int mode, NoiseCipherState *sa, NoiseCipherState *sb, uint8_
                 break;
             }
             rc = launch_ragged(mode != W_SEAL, a, d_wire, (NoiseAeadRecord *)(sg->d + k->meta_off),
-                               sg->d + k->status_off, n, sg->stream);
+                               sg->d + k->status_off, n, k->max_len, sg->stream);
             if (rc) break;
             hipError_t e;
             if (mode == W_SEAL) { /* nothing to gate: the whole chunk comes back,
@@ -319,7 +324,7 @@ static int wire_run(int mode, NoiseCipherState *sa, NoiseCipherState *sb, uint8_
                     e = hipStreamWaitEvent(sg->stream_out, sg->ev_out[gated], 0);
                     if (e == hipSuccess && mode == W_ECHO &&
                         launch_ragged(0, b, d_wire, (NoiseAeadRecord *)(sg->d + k->desc_b_off), NULL,
-                                      p, sg->stream_out))
+                                      p, k->max_len, sg->stream_out))
                         e = hipErrorLaunchFailure;
                     if (e == hipSuccess)
                         e = hipMemcpyAsync(h_wire + k->w0, d_wire + k->w0, pend - k->w0,

@@ -105,7 +105,7 @@ LENS = [0, 1, 15, 16, 17, 48, 56, 63, 64, 65, 127, 128, 129, 191, 192, 255, 256,
 
 
 @pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 2), (CHACHA, 4), (CHACHA, 8),
-                                          (AES, 0)])
+                                          (CHACHA, 16), (CHACHA, 32), (CHACHA, 64), (AES, 0)])
 @pytest.mark.parametrize("packed", [False, True])
 @pytest.mark.parametrize("rps", [13, 16])
 def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed, rps):
@@ -179,7 +179,8 @@ def test_uniform_staged_kernels(aead, gpu, oracle, cipher):
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L]), f"len={L} rec={i}"
 
 
-@pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 4), (CHACHA, 8), (AES, 0)])
+@pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 4), (CHACHA, 8), (CHACHA, 32),
+                                          (CHACHA, 64), (AES, 0)])
 @pytest.mark.parametrize("rps", [4, 16])
 def test_uniform_with_ad(aead, gpu, oracle, cipher, lanes, rps):
     rng = np.random.default_rng(77 + lanes + rps)
@@ -218,7 +219,7 @@ def test_max_record(aead, gpu, oracle):
     """NOISE_MAX_PAYLOAD_LEN - 16 bytes of plaintext (constants.h:151)."""
     rng = np.random.default_rng(9)
     L = 65535 - 16
-    for cipher, lanes in [(CHACHA, 8), (CHACHA, 1), (AES, 0)]:
+    for cipher, lanes in [(CHACHA, 8), (CHACHA, 1), (CHACHA, 16), (CHACHA, 64), (AES, 0)]:
         keys = rng.integers(0, 256, (1, 32), dtype=np.uint8)
         pt = rng.integers(0, 256, 2 * L, dtype=np.uint8)
         exp = oracle_seal_records(oracle, cipher, keys, [123], 2, pt, L, L, 2, L + 16)
@@ -260,9 +261,11 @@ def test_in_place(aead, gpu, oracle):
 
 # ------------------------------------------------------------ ragged kernel
 
-@pytest.mark.parametrize("cipher", [CHACHA, AES])
-def test_ragged_vs_oracle(aead, gpu, oracle, cipher):
-    rng = np.random.default_rng(21 + (cipher & 3))
+@pytest.mark.parametrize("cipher,lanes", [(CHACHA, 0), (CHACHA, 4), (CHACHA, 8), (CHACHA, 16),
+                                          (CHACHA, 32), (CHACHA, 64), (AES, 0), (AES, 4)])
+def test_ragged_vs_oracle(aead, gpu, oracle, cipher, lanes):
+    """lanes 0: the library's choice (wide groups for a batch this small)."""
+    rng = np.random.default_rng(21 + (cipher & 3) + lanes)
     S, count = 5, 200
     keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
     torch = _torch()
@@ -294,7 +297,7 @@ def test_ragged_vs_oracle(aead, gpu, oracle, cipher):
     d_out = torch.full((inp_size,), 0xA5, dtype=torch.uint8, device="cuda")
     rc = aead.dev_ragged(False, cipher, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
                          inp=d_in.data_ptr(), out=d_out.data_ptr(), n_records=count,
-                         ad=d_ad.data_ptr(), stream=stream())
+                         ad=d_ad.data_ptr(), lanes=lanes, stream=stream())
     assert rc == 0
     sync()
     got = d_out.cpu().numpy()
@@ -306,7 +309,7 @@ def test_ragged_vs_oracle(aead, gpu, oracle, cipher):
     d_st = torch.full((count,), 9, dtype=torch.uint8, device="cuda")
     rc = aead.dev_ragged(True, cipher, ctx_base=ctx.data_ptr(), recs=d_recs2.data_ptr(),
                          inp=d_out.data_ptr(), out=d_out.data_ptr(), n_records=count,
-                         ad=d_ad.data_ptr(), status=d_st.data_ptr(), stream=stream())
+                         ad=d_ad.data_ptr(), status=d_st.data_ptr(), lanes=lanes, stream=stream())
     assert rc == 0
     sync()
     assert np.all(d_st.cpu().numpy() == 0)
@@ -316,17 +319,19 @@ def test_ragged_vs_oracle(aead, gpu, oracle, cipher):
         assert np.array_equal(back[o: o + L], inp[io: io + L])
 
 
-@pytest.mark.parametrize("cipher", [CHACHA, AES])
+@pytest.mark.parametrize("cipher,lanes", [(CHACHA, 0), (CHACHA, 4), (CHACHA, 8), (AES, 4),
+                                          (AES, 0)])
 @pytest.mark.parametrize("fast", [True, False])
-def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, fast):
+def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, lanes, fast):
     """Many workgroup windows (records taken in length order inside each),
     per-state record runs of uneven size (so some windows hold 2 states,
     some 3+: the AES LDS state slots and the global-context path), 1/2 of
     the records in place, every 37th record tampered: each status, each
     verified plaintext and each rejected record's untouched bytes must match
-    the oracle."""
+    the oracle.  lanes 0 is the library's choice for a batch this small:
+    64-lane ChaChaPoly groups, one AES-GCM record per workgroup (gcm_wide)."""
     torch = _torch()
-    rng = np.random.default_rng(77 + (cipher & 3) + 10 * fast)
+    rng = np.random.default_rng(77 + (cipher & 3) + 10 * fast + lanes)
     count = 1500
     runs = []
     while sum(runs) < count:
@@ -356,7 +361,7 @@ def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, fast):
     flags = aead.FLAG_FAST if fast else 0
     assert aead.dev_ragged(False, cipher, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
                            inp=d_buf.data_ptr(), out=d_buf.data_ptr(), n_records=count,
-                           flags=flags, stream=stream()) == 0
+                           flags=flags, lanes=lanes, stream=stream()) == 0
     sync()
     sealed = d_buf.cpu().numpy().copy()
     for i in list(range(0, count, 7)) + [count - 1]:
@@ -372,7 +377,7 @@ def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, fast):
     d_st = torch.full((count,), 9, dtype=torch.uint8, device="cuda")
     assert aead.dev_ragged(True, cipher, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
                            inp=d_buf.data_ptr(), out=d_buf.data_ptr(), n_records=count,
-                           status=d_st.data_ptr(), flags=flags, stream=stream()) == 0
+                           status=d_st.data_ptr(), flags=flags, lanes=lanes, stream=stream()) == 0
     sync()
     st = d_st.cpu().numpy()
     back = d_buf.cpu().numpy()

@@ -1,0 +1,6 @@
+#!/bin/sh
+# Builds tools/latency (single-record GPU CipherState latency, tools/latency.c).
+set -e
+cd "$(dirname "$0")/.."
+gcc -O2 -Iinclude tools/latency.c -Lnoise-c_amd/lib -lnoise_aead_hip \
+    -Wl,-rpath,'$ORIGIN/../noise-c_amd/lib' -o tools/latency
