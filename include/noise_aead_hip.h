@@ -186,7 +186,7 @@ int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_
  *       1 (MAC failure, nothing written).  in == out (in place) is allowed.
  * lanes_per_record: 0 = automatic; ChaChaPoly 1, 2, 4, 8, 16, 32 or 64 (wider
  * groups cut the latency of small batches of long records); AESGCM 4 (0 lets
- * a ragged batch of at most 4096 records run one record per workgroup). */
+ * a ragged batch of at most 512 records run one record per workgroup). */
 typedef struct NoiseAeadUniform {
     const void *ctx;
     const uint64_t *nonce_base;

@@ -10,6 +10,8 @@
 #include "aead_kernels.h"
 #include <hip/hip_runtime.h>
 #include <mutex>
+#include <cstdlib>
+#include <cstring>
 
 
 #include "chachapoly.hip"
@@ -42,14 +44,20 @@ hipError_t ensure_aes_tables(hipStream_t stream)
 }
 
 /* Lanes per record for ChaChaPoly: 4 (the fastest split at 64 Ki and 1 Mi
-   records, profiles/r01_sweep_*); a batch too small to give every SIMD four
-   waves that way gets wider groups, up to one wave per record — that is the
+   records, profiles/r01_sweep_*), 8 when the batch is too small to give
+   every SIMD four waves that way.  Batches of at most WIDE_MAX_RECORDS — the
    single-call latency path, where a long record's blocks would otherwise run
-   serially on a few lanes.  No wider than the longest record needs (two
-   ChaCha blocks per lane); max_len = 0 when unknown (device descriptors). */
+   serially on a few lanes — get wider groups, up to one wave per record, but
+   no wider than the longest record needs (two ChaCha blocks per lane;
+   max_len = 0 when unknown).  Larger pipelined chunks (≈ 3 K records of
+   1400 B) measured faster at 8 (profiles/r01_hostpaths_ab). */
+constexpr uint32_t WIDE_MAX_RECORDS = 512;
+
 int auto_lanes(uint32_t n_records, uint32_t max_len)
 {
     const uint64_t target = 256ull * 16 * 64; /* 4 waves on each of 1024 SIMDs */
+    if (n_records > WIDE_MAX_RECORDS) /* throughput regime: 4, or 8 below 64 Ki */
+        return (uint64_t)n_records * 4 < target ? 8 : 4;
     int k = 4;
     while (k < 64 && (uint64_t)n_records * k < target) k <<= 1;
     if (max_len) {
@@ -226,7 +234,7 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
         /* LDS-staged kernel: 1024-thread workgroups over 256-record windows;
            a batch too small to give every CU one of those uses 256-thread
            workgroups over 64-record windows instead (4x the workgroups) */
-        if (job->lanes_per_record == 0 && job->n_records <= GCM_WIDE_MAX_RECORDS) {
+        if (job->lanes_per_record == 0 && job->n_records <= WIDE_MAX_RECORDS) {
             /* small batch: a workgroup per record (latency, not throughput);
                lanes_per_record = 4 keeps the windowed 4-lane kernels */
             hipLaunchKernelGGL(open ? gcm_wide<true> : gcm_wide<false>, dim3(job->n_records),
@@ -440,10 +448,29 @@ int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)
     return 0;
 }
 
+/* NOISE_AEAD_LANES=narrow: the host paths keep K <= 8 and the 4-lane AES
+   kernels (an A/B switch for measurements). */
+static bool lanes_narrow()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("NOISE_AEAD_LANES");
+        v = e && strcmp(e, "narrow") == 0;
+    }
+    return v != 0;
+}
+
 /* host_internal.h: the host paths know their records' lengths */
 __attribute__((visibility("hidden"))) uint32_t na_chacha_lanes(uint32_t n_records, uint32_t max_len)
 {
+    if (lanes_narrow()) return (uint64_t)n_records * 4 < 256ull * 16 * 64 ? 8 : 4;
     return (uint32_t)auto_lanes(n_records, max_len ? max_len : 1);
+}
+
+__attribute__((visibility("hidden"))) uint32_t na_aes_lanes(uint32_t n_records)
+{
+    (void)n_records;
+    return lanes_narrow() ? GCM_LANES : 0;
 }
 
 } // extern "C"

@@ -799,16 +799,13 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
 
 /* ------------------------------------------ wide (small batches, latency)
  *
- * One record per 256-thread workgroup, for batches too small to fill the
- * chip four lanes per record (the single-call path of noise_cipherstate_*,
- * short wire buffers).  The record's CTR blocks are spread over all 256
+ * One record per 256-thread workgroup, for batches of at most 512 records
+ * (the single-call path of noise_cipherstate_*, short wire buffers).  The record's CTR blocks are spread over all 256
  * threads; GHASH is gcm_record's 4-lane Horner (H^4 steps, scale by
  * H^(4-l), XOR-reduce) run by lanes 0..3 with the H^4 table in LDS.  Seal:
  * CTR, then GHASH over the CT just written.  Open: GHASH and tag check
  * first, CTR only when the tag verified (cipher-aesgcm.c:184-186).
  */
-constexpr uint32_t GCM_WIDE_MAX_RECORDS = 4096; /* aead_api.hip run_ragged */
-
 template <bool OPEN>
 __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
 {
@@ -841,9 +838,7 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
             for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
             store16(dst + 16 * b, nb, x);
         }
-        __threadfence(); /* the GHASH lanes read this CT back */
-        __syncthreads();
-        __threadfence();
+        __syncthreads(); /* the GHASH lanes read this CT back (same CU) */
     }
     if (t < (uint32_t)K) {
         const int l = (int)t;

@@ -323,7 +323,7 @@ static int launch_chunk(Staging *sg, const Chunk *c, int ci, int open, int zc)
         job.ad = base;
         job.status = base + c->status_off + first;
         job.n_records = count;
-        job.lanes_per_record = k == 0 ? na_chacha_lanes(count, c->chacha_max_len) : 0;
+        job.lanes_per_record = k == 0 ? na_chacha_lanes(count, c->chacha_max_len) : na_aes_lanes(count);
         job.flags = NOISE_AEAD_FLAG_FAST;
         job.reserved_ = 0;
         int cid = k == 0 ? NOISE_CIPHER_CHACHAPOLY : NOISE_CIPHER_AESGCM;

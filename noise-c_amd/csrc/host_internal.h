@@ -73,6 +73,7 @@ NA_HIDDEN int na_is_ours(const NoiseCipherState *st);
 NA_HIDDEN void na_clean(void *p, size_t n);
 /* ChaChaPoly lanes per record for n records of at most max_len bytes (aead_api.hip) */
 NA_HIDDEN uint32_t na_chacha_lanes(uint32_t n_records, uint32_t max_len);
+NA_HIDDEN uint32_t na_aes_lanes(uint32_t n_records); /* 0 (automatic) or 4 */
 /* memcpy with non-temporal (streaming) stores: staging copies are written
    once and read back by DMA or by another pass much later, so skipping the
    read-for-ownership of every destination line halves their write traffic */

@@ -152,7 +152,7 @@ static int launch_ragged(int open, const HipCipherState *st, const uint8_t *d_ba
     job.status = d_status;
     job.n_records = (uint32_t)n;
     job.lanes_per_record = st->parent.cipher_id == NOISE_CIPHER_CHACHAPOLY
-                               ? na_chacha_lanes((uint32_t)n, max_len) : 0;
+                               ? na_chacha_lanes((uint32_t)n, max_len) : na_aes_lanes((uint32_t)n);
     job.flags = 0; /* frames sit at 2-byte offsets: the any-alignment kernels */
     job.reserved_ = 0;
     return open ? noise_aead_dev_open_ragged(st->parent.cipher_id, &job, s)
