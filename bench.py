@@ -197,15 +197,18 @@ def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length):
     return f"chachapoly_seal_uniform<{lanes}, {'true' if fast else 'false'}>"
 
 
-def load_pmc(config_name: str, kernel: str):
+def load_pmc(config_name: str, kernel: str, scale: float = 1.0):
     """Per-launch PMC counters of `kernel` from profiles/traffic_<cfg>.json
-    (tools/gpu/pmc.sh + tools/pmc_report.py), or {}."""
+    (tools/gpu/pmc.sh + tools/pmc_report.py, collected at N = 1), or {}.
+    `scale`: this launch's share of the profiled one (1/N for a strong-scaling
+    shard; the counters are per-launch totals proportional to the records)."""
     path = os.path.join(ROOT, "profiles", f"traffic_{config_name}.json")
     if not os.path.exists(path):
         return {}
     with open(path) as f:
         t = json.load(f)
-    return t.get("kernels", {}).get(kernel) or {}
+    k = t.get("kernels", {}).get(kernel) or {}
+    return {n: v * scale for n, v in k.items()} if scale != 1.0 else k
 
 
 # VALU issue ceiling (DESIGN.md §5): a SIMD issues one wave64 integer VALU
@@ -364,7 +367,7 @@ def main():
     alg_seal = N * (2 * L + 16 + AD) + len(sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
     achieved = alg_seal / (seal_ms * 1e-3) / 1e9
     kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L)
-    pmc = load_pmc(args.config, kname)
+    pmc = load_pmc(args.config, kname, 1.0 / world if cfg.get("strong") else 1.0)
     traffic = pmc.get("hbm_bytes_per_launch")
     result = {
         "metric": (f"GiB/s device-resident AEAD encrypt+decrypt, {N * world // 1024}Ki x {L}B "
