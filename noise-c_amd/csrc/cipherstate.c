@@ -200,7 +200,6 @@ typedef struct {
     Job *jobs;
     uint8_t *h;
     int open;
-    size_t base;   /* byte range for the scrub step */
 } CopyArg;
 
 static void pack_range(void *p, size_t lo, size_t hi)
@@ -214,19 +213,19 @@ static void pack_range(void *p, size_t lo, size_t hi)
     }
 }
 
+/* Copy committed results out.  Open: every slot the GPU wrote plaintext into
+   (a verified record, committed or deferred) is zeroed right after, while its
+   lines are still in cache — failed records hold only their ciphertext, so no
+   second pass over the whole staging area is needed. */
 static void unpack_range(void *p, size_t lo, size_t hi)
 {
     CopyArg *a = (CopyArg *)p;
     for (size_t k = lo; k < hi; ++k) {
         const Job *j = &a->jobs[k];
         if (j->commit) memcpy(j->data, a->h + j->off, j->len + (a->open ? 0 : 16));
+        if (a->open && !j->skip && j->status == NOISE_ERROR_NONE)
+            explicit_bzero(a->h + j->off, j->len);
     }
-}
-
-static void scrub_range(void *p, size_t lo, size_t hi)
-{
-    CopyArg *a = (CopyArg *)p;
-    explicit_bzero(a->h + a->base + lo, hi - lo);
 }
 
 static size_t copy_grain(const Chunk *c, size_t n)
@@ -356,11 +355,10 @@ static int finish_chunk(Staging *sg, Job *jobs, const Chunk *c, int ci, int open
         if (!decide) j->commit = j->status == NOISE_ERROR_NONE;
     }
     if (decide) decide(jobs, c->j0, c->j1, u);
-    CopyArg a = {jobs + c->j0, sg->h, open, c->payload_off};
-    host_pool_for(c->j1 - c->j0, copy_grain(c, c->j1 - c->j0), unpack_range, &a);
+    CopyArg a = {jobs + c->j0, sg->h, open};
     /* after seal the slots hold only CT || tag (the D2H overwrote every
-       staged plaintext byte); after open they hold verified plaintext */
-    if (open) host_pool_for(c->end - c->payload_off, (size_t)1 << 20, scrub_range, &a);
+       staged plaintext byte); after open unpack_range zeroes the plaintext */
+    host_pool_for(c->j1 - c->j0, copy_grain(c, c->j1 - c->j0), unpack_range, &a);
     return NOISE_ERROR_NONE;
 }
 
@@ -430,7 +428,7 @@ static int run_jobs(Job *jobs, size_t n, int open, decide_fn decide, void *u)
         const Chunk *ch = &chunks[c];
         if (tr) t0 = na_now_ms();
         fill_descriptors(jobs, ch, sg->h);
-        CopyArg a = {jobs + ch->j0, sg->h, open, 0};
+        CopyArg a = {jobs + ch->j0, sg->h, open};
         host_pool_for(ch->j1 - ch->j0, copy_grain(ch, ch->j1 - ch->j0), pack_range, &a);
         if (tr) t_pack += na_now_ms() - t0;
         /* AES-GCM's GHASH lanes read the CT serially: over PCIe that only

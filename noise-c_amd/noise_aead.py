@@ -15,7 +15,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libnoise_aead_hip.so")
+# NOISE_AEAD_LIB: another build of the same ABI (A/B measurements only)
+LIB_PATH = os.environ.get("NOISE_AEAD_LIB") or os.path.join(HERE, "lib", "libnoise_aead_hip.so")
 HEADER = os.path.join(HERE, "..", "include", "noise_aead_hip.h")
 
 
