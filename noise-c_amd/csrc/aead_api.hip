@@ -173,6 +173,7 @@ UniformArgs to_args(const NoiseAeadUniform *j)
     a.n_records = j->n_records;
     a.len = j->len;
     a.ad_len = j->ad_len;
+    a.balance = 0;
     return a;
 }
 
@@ -181,12 +182,14 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     int rc = check_uniform(job);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
-    const UniformArgs a = to_args(job);
+    UniformArgs a = to_args(job);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
         const bool ukey = k >= 4 && job->recs_per_state % (64u / (uint32_t)k) == 0;
         KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open), ukey);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
+        /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC) */
+        a.balance = (uint64_t)job->n_records * (uint32_t)k <= 4096ull * 64;
         return launch(fn, job->n_records, k, a, s);
     }
     if (cipher_id == NOISE_CIPHER_AESGCM) {
