@@ -388,4 +388,28 @@ NA_DEV void mask_unit(uint32_t w[16], uint32_t n)
     }
 }
 
+/* Issue priority by progress.  A SIMD's VALU slots go to the highest
+   priority, then the OLDEST wave (MI355X_MICROARCH.md, "Two waves per SIMD"
+   item 2), so the 4 waves a SIMD holds in a C2-sized batch — one resident
+   generation — ran nearly one after another: they finished at ~20, 36, 50
+   and 66 us, the last ~30 us with only 1-2 waves left to hide latency
+   (profiles/r01_timeline_c2.log).  Lowering a wave's priority as it gets
+   ahead (done = steps finished, of total) lets the others catch up, so all
+   four stay resident to the end.  Used by the open kernel when the batch is
+   one generation (UniformArgs.balance): +3.5 % open at C2, while at C4
+   (16 generations) and in the seal kernel it measured neutral to -3 %
+   (profiles/r01_prio_ab.jsonl); in the LDS-bound AES-GCM staged kernel it
+   cost 4.6 % at C3 and is not used there.  Wave-uniform arguments: scalar
+   branches. */
+NA_DEV void prio_by_progress(uint32_t done, uint32_t total)
+{
+#ifndef NA_NO_PRIO_BALANCE
+    const uint32_t q = (4 * done) / (total ? total : 1);
+    if (q == 0) __builtin_amdgcn_s_setprio(3);
+    else if (q == 1) __builtin_amdgcn_s_setprio(2);
+    else if (q == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
 } // namespace na

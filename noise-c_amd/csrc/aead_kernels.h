@@ -23,7 +23,7 @@ struct UniformArgs {
     uint64_t in_stride, out_stride, ad_stride;
     uint32_t rps, n_records, len, ad_len;
     uint32_t balance;           /* the whole batch is one resident generation
-                                   of waves (chachapoly.hip prio_by_progress) */
+                                   of waves (aead_device.h prio_by_progress) */
 };
 
 /* Ragged batch: one descriptor per record (variable lengths, states, AD).
