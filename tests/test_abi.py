@@ -178,3 +178,15 @@ def test_batch_host_rules(aead_built):
     assert rc == 0 and res == [0, A.ERROR_INVALID_LENGTH, A.ERROR_INVALID_NONCE]
     nokey.free()
     spent.free()
+
+
+def test_default_lane_policy(aead_built):
+    """Lanes per record the library picks (aead_api.hip auto_lanes): 4 at the
+    BASELINE sizes, 8 below 64 Ki records, and wide groups (up to a wave per
+    record) only for batches of at most 512 records — the latency regime."""
+    A = aead_built
+    lanes = lambda n: A.dev_default_lanes(A.CHACHAPOLY, n)
+    assert lanes(65536) == 4 and lanes(1 << 20) == 4
+    assert lanes(65535) == 8 and lanes(513) == 8
+    assert lanes(512) == 64 and lanes(1) == 64
+    assert A.dev_default_lanes(A.AESGCM, 1) == 4
