@@ -739,11 +739,13 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
     return true;
 }
 
-/* the cold path: a record whose state has no LDS slot (kept out of line so
-   its register needs do not weigh on the slot path) */
+/* the cold path: a record whose state has no LDS slot.  Inlined: as an
+   out-of-line call its frame and caller-saved registers cost the slot path
+   scratch traffic (open 176 -> 104 B/lane, seal 64 -> 0) and C5's AES
+   kernels 2-5 % (profiles/r01_aes_inline_ab.jsonl). */
 template <bool OPEN, bool FAST>
-__device__ __attribute__((noinline)) bool gcm_record_global(const GcmView &rv, int l,
-                                                            const uint8_t *TE, uint32_t tpl)
+__device__ __forceinline__ bool gcm_record_global(const GcmView &rv, int l,
+                                                  const uint8_t *TE, uint32_t tpl)
 {
     return gcm_record_staged<OPEN, FAST>(rv, l, TE, tpl, rv.ctx->rk,
                                          (const uint4 *)rv.ctx->tab[GCM_LANES - 1]);
