@@ -43,6 +43,8 @@
 
 namespace na {
 
+typedef __attribute__((address_space(3))) void lds_void;
+
 /* One record as seen by its group of lanes. */
 struct RecView {
     const uint8_t *src;
@@ -362,8 +364,28 @@ NA_DEV void seal_il(const RecView &rv, int k)
     if (k == K - 1) tail_out<FAST, true>(rv.dst, g.J, len, w, tag);
 }
 
-template <int K, bool FAST>
-NA_DEV bool open_il(const RecView &rv, int k)
+/* Open's authentication pass has only Poly1305 (≈200 instructions per unit)
+   to hide each unit's load behind, so with one unit prefetched in registers
+   it waits on memory.  The FAST ragged kernels stream it through a ring of
+   three 4 KB LDS tiles per wave instead (LDS-DMA, two units in flight, no
+   VGPRs): three distinct arrays, so each unrolled step's tile is static and
+   the reads wait only for their own tile's DMA. */
+struct AuthRing { uint4 *t0, *t1, *t2; };
+
+template <int K>
+NA_DEV void auth_dma(const RecView &rv, const GroupCtx<K> &g, int k, uint32_t m, uint4 *t)
+{
+    const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
+    const bool ok = m < g.steps && v >= 1; /* else unit 0: FAST slots are readable */
+    const uint8_t *p = rv.src + 64u * (ok ? (uint32_t)v - 1 : 0u);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        __builtin_amdgcn_global_load_lds((const void *)(p + 16 * c), (lds_void *)(t + 64 * c),
+                                         16, 0, 0);
+}
+
+template <int K, bool FAST, bool RING = false>
+NA_DEV bool open_il(const RecView &rv, int k, AuthRing ring = AuthRing{})
 {
     uint32_t key[8];
     load_key(rv.key, key);
@@ -389,6 +411,52 @@ NA_DEV bool open_il(const RecView &rv, int k)
     /* phase 1: authenticate the ciphertext */
     uint32_t wn[16], wc[16];
     bool seen = false;
+    if constexpr (RING) {
+        static_assert(FAST, "the LDS ring reads whole units");
+        const uint32_t lane = threadIdx.x & 63;
+        /* step m: DMA step m+2 into the tile step m-1 used, wait for step m's
+           four loads (8 newer ones may stay in flight), Poly over the unit */
+        auto step = [&](uint32_t m, const uint4 *cur, uint4 *nxt) {
+            auth_dma<K>(rv, g, k, m + 2, nxt);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            /* the tile is read by hand: the compiler cannot tell which tile an
+               LDS-DMA fills and would wait for all of them (vmcnt(0)) */
+            uint32_t w[16];
+            const uint32_t addr = (uint32_t)(uintptr_t)(const lds_void *)(cur + lane);
+            uint4 q0, q1, q2, q3;
+            asm volatile("ds_read_b128 %0, %4\n"
+                         "ds_read_b128 %1, %4 offset:1024\n"
+                         "ds_read_b128 %2, %4 offset:2048\n"
+                         "ds_read_b128 %3, %4 offset:3072\n"
+                         "s_waitcnt lgkmcnt(0)"
+                         : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3) : "v"(addr) : "memory");
+            w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w;
+            w[4] = q1.x; w[5] = q1.y; w[6] = q1.z; w[7] = q1.w;
+            w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
+            w[12] = q3.x; w[13] = q3.y; w[14] = q3.z; w[15] = q3.w;
+            const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
+            if (v >= 1) {
+                const uint32_t j = (uint32_t)v - 1;
+                uint32_t nb = 4;
+                if (j + 1 == g.J) {
+                    const uint32_t bytes = len - 64 * j;
+                    mask_unit(w, bytes);
+                    nb = (bytes + 15) / 16;
+                }
+                poly_unit(acc, seen ? mjump : mr, mr, w, nb);
+                seen = true;
+            }
+            __builtin_amdgcn_wave_barrier(); /* all lanes read cur before it is refilled */
+        };
+        auth_dma<K>(rv, g, k, 0, ring.t0);
+        auth_dma<K>(rv, g, k, 1, ring.t1);
+        for (uint32_t m = 0; m < g.steps; m += 3) {
+            step(m, ring.t0, ring.t2);
+            if (m + 1 < g.steps) step(m + 1, ring.t1, ring.t0);
+            if (m + 2 < g.steps) step(m + 2, ring.t2, ring.t1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no DMA outlives the pass */
+    } else {
 #pragma unroll
     for (int i = 0; i < 16; ++i) wn[i] = 0;
     unit_prefetch<FAST>(rv.src, v0 >= 1, (uint32_t)v0 - 1, len, wn);
@@ -409,6 +477,7 @@ NA_DEV bool open_il(const RecView &rv, int k)
             poly_unit(acc, seen ? mjump : mr, mr, wc, nb);
             seen = true;
         }
+    }
     }
     uint32_t tag[4], got[4];
     poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
@@ -536,8 +605,6 @@ NA_DEV Quad wave_load(const UniformArgs &a, const WaveIO<K> &io, int j0)
     P.d = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 3), last) * a.in_stride + off);
     return P;
 }
-
-typedef __attribute__((address_space(3))) void lds_void;
 
 /* The same step as wave_load, but straight into the tile by LDS-DMA
    (global_load_lds_dwordx4: no VGPRs, no ds_write).  The DMA fills the tile
@@ -1110,7 +1177,14 @@ __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
                                              threadIdx.x / K, order);
     if (rec >= a.n_records) return;
     const int k = (int)(threadIdx.x % K);
-    const bool ok = open_any<K, FAST>(ragged_view(a, rec), k);
+    bool ok;
+    if constexpr (FAST && K >= 4) {
+        __shared__ uint4 r0[4][256], r1[4][256], r2[4][256]; /* 3 x 4 KB per wave */
+        const uint32_t w = threadIdx.x >> 6;
+        ok = open_il<K, true, true>(ragged_view(a, rec), k, AuthRing{r0[w], r1[w], r2[w]});
+    } else {
+        ok = open_any<K, FAST>(ragged_view(a, rec), k);
+    }
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
