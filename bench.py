@@ -242,6 +242,8 @@ def main():
     ap.add_argument("--no-xfer", action="store_true",
                     help="skip the N>1 scatter/seal/gather leg (RCCL, SURVEY.md 8e)")
     ap.add_argument("--xfer-reps", type=int, default=5)
+    ap.add_argument("--streams", type=int, default=1, choices=(1, 2),
+                    help="C2-C4/perf: 2 = consecutive steps alternate between two streams")
     ap.add_argument("--c5-streams", type=int, default=2, choices=(1, 2),
                     help="C5: 2 = the AES-GCM and ChaChaPoly halves on two streams, concurrently")
     args = ap.parse_args()
@@ -308,21 +310,28 @@ def main():
 
     lanes = args.lanes or A.dev_default_lanes(cipher, N)
 
-    def seal(b, pt=None, ct=None):
+    def seal(b, pt=None, ct=None, stream=sp):
         if pt is None:
             pt, ct, _, _ = sets[b]
         return A.dev_uniform(False, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
                              inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
                              out_stride=out_stride, length=L, n_records=N,
-                             recs_per_state=sh["rps"], lanes=lanes, stream=sp, **ad_kw)
+                             recs_per_state=sh["rps"], lanes=lanes, stream=stream, **ad_kw)
 
-    def open_(b):
+    def open_(b, stream=sp):
         _, ct, back, st = sets[b]
         return A.dev_uniform(True, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
                              inp=ct.data_ptr(), out=back.data_ptr(), in_stride=out_stride,
                              out_stride=in_stride, length=L, n_records=N,
                              recs_per_state=sh["rps"], status=st.data_ptr(), lanes=lanes,
-                             stream=sp, **ad_kw)
+                             stream=stream, **ad_kw)
+
+    # --streams 2: consecutive steps (independent batch sets) alternate between
+    # two streams, so step s+1's seal can start on CUs that step s's open is
+    # leaving (a server pipelining independent batches).  Each step's seal ->
+    # open stays ordered on its own stream; set b is reused only every
+    # `sets` steps, on the same stream.
+    streams = [stream] + ([torch.cuda.Stream(dev)] if args.streams == 2 else [])
 
     for w in range(args.warmup):
         assert seal(w % args.sets) == 0
@@ -336,11 +345,12 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         b = s % args.sets
-        ev[s][0].record(stream)
-        rc1 = seal(b)
-        ev[s][1].record(stream)
-        rc2 = open_(b)
-        ev[s][2].record(stream)
+        st_ = streams[s % len(streams)]
+        ev[s][0].record(st_)
+        rc1 = seal(b, stream=st_.cuda_stream)
+        ev[s][1].record(st_)
+        rc2 = open_(b, stream=st_.cuda_stream)
+        ev[s][2].record(st_)
         if rc1 or rc2:
             raise RuntimeError(f"launch failed {rc1:#x} {rc2:#x}")
     torch.cuda.synchronize(dev)
@@ -353,6 +363,21 @@ def main():
 
     seal_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
     open_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    if len(streams) > 1:
+        # overlapped launches stretch each other's events: the per-launch
+        # times of the roofline come from a serial, untimed pass instead
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        reps = 5
+        e[0].record(stream)
+        for r in range(reps):
+            seal(r % args.sets)
+        e[1].record(stream)
+        for r in range(reps):
+            open_(r % args.sets)
+        e[2].record(stream)
+        torch.cuda.synchronize(dev)
+        seal_ms = e[0].elapsed_time(e[1]) / reps
+        open_ms = e[1].elapsed_time(e[2]) / reps
 
     ok = True
     if args.verify:
@@ -389,7 +414,8 @@ def main():
         "config": {"workload": cfg["workload"], "config": args.config, "records_per_gpu": N,
                    "record_len": L, "states_per_gpu": S, "lanes_per_record": lanes,
                    "in_stride": in_stride, "out_stride": out_stride,
-                   "payload_bytes_per_step": int(payload_step), "parallelism": f"records x{world}"},
+                   "payload_bytes_per_step": int(payload_step), "parallelism": f"records x{world}",
+                   "streams": len(streams)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": kname,
