@@ -190,3 +190,29 @@ def test_default_lane_policy(aead_built):
     assert lanes(65535) == 8 and lanes(513) == 8
     assert lanes(512) == 64 and lanes(1) == 64
     assert A.dev_default_lanes(A.AESGCM, 1) == 4
+
+
+def test_device_api_argument_rules(aead_built):
+    """The device-resident entry points reject bad jobs before any HIP call
+    (aead_api.hip check_uniform / run_ragged), so these run without a GPU.
+    The pointers are never dereferenced: every case fails validation."""
+    A = aead_built
+    fake = 1 << 20  # aligned, non-null, never touched
+    ok = dict(ctx=fake, nonce_base=fake, inp=fake, out=fake, in_stride=1408, out_stride=1424,
+              length=1400, n_records=4, recs_per_state=4)
+    for open_ in (False, True):
+        for cid in (A.CHACHAPOLY, A.AESGCM):
+            assert A.dev_uniform(open_, cid, **{**ok, "nonce_base": 0}) == A.ERROR_INVALID_PARAM
+            assert A.dev_uniform(open_, cid, **{**ok, "recs_per_state": 0}) == A.ERROR_INVALID_PARAM
+            assert A.dev_uniform(open_, cid, **{**ok, "ctx": fake + 8}) == A.ERROR_INVALID_PARAM
+            assert A.dev_uniform(open_, cid, **{**ok, "ad_len": 32}) == A.ERROR_INVALID_PARAM
+            assert A.dev_uniform(open_, cid, **{**ok, "length": 65520}) == A.ERROR_INVALID_LENGTH
+        assert A.dev_uniform(open_, A.CHACHAPOLY, **{**ok, "lanes": 3}) == A.ERROR_INVALID_PARAM
+        assert A.dev_uniform(open_, A.AESGCM, **{**ok, "lanes": 8}) == A.ERROR_INVALID_PARAM
+        assert A.dev_uniform(open_, A.CHACHAPOLY, **{**ok, "n_records": 0}) == 0
+        rg = dict(ctx_base=0, recs=fake, inp=fake, out=fake, n_records=4)
+        for cid in (A.CHACHAPOLY, A.AESGCM):
+            assert A.dev_ragged(open_, cid, **{**rg, "recs": 0}) == A.ERROR_INVALID_PARAM
+            assert A.dev_ragged(open_, cid, **{**rg, "out": 0}) == A.ERROR_INVALID_PARAM
+        assert A.dev_ragged(open_, A.CHACHAPOLY, **{**rg, "lanes": 5}) == A.ERROR_INVALID_PARAM
+        assert A.dev_ragged(open_, 0x4399, **rg) == A.ERROR_UNKNOWN_ID
