@@ -1,0 +1,85 @@
+"""Full-size golden digests of the bench workloads.
+
+Test infrastructure: runs the CPU oracle (oracle/_build/liboracle.so, pinned
+against the reference's own vectors in tests/test_oracle.py) over the exact
+synthetic inputs bench.py generates at N = 1 (SplitMix64
+plaintext of seed 0x7074 over the strided input slots, keys of seed 0x6B6579
+at word 4*key_id, nonce base 0) and records, per config, the SHA-256 of the
+packed plaintexts (pins the generator) and of the packed sealed records
+(ct || tag, record after record, stride padding excluded).
+
+    python tests/golden/gen_config_digests.py   ->  tests/golden/config_digests.json
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+from oracle import REF_SO, Oracle, RefLib  # noqa: E402
+
+CHACHA, AES = 0x4301, 0x4302
+SEED_PT, SEED_KEY = 0x7074, 0x6B6579
+ALIGN = 16
+# bench.py CONFIGS at N = 1 (C5 is ragged and covered by its own tests)
+CONFIGS = {
+    "c2": dict(cipher=CHACHA, records=65536, len=1400, states=1),
+    "c3": dict(cipher=AES, records=65536, len=1400, states=1),
+    "c4": dict(cipher=CHACHA, records=1048576, len=1400, states=4096),
+}
+
+
+def stride(n):
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+def digests(o, name, cfg):
+    N, L, S = cfg["records"], cfg["len"], cfg["states"]
+    ins, outs = stride(L), stride(L + 16)
+    keys = np.frombuffer(b"".join(o.fill(SEED_KEY, 32, 4 * k) for k in range(S)), dtype=np.uint8).copy()
+    nb = np.zeros(S, dtype=np.uint64)
+    pt = np.frombuffer(o.fill(SEED_PT, N * ins, 0), dtype=np.uint8).copy()
+    ct = np.zeros(N * outs, dtype=np.uint8)
+    o.seal_uniform(cfg["cipher"], keys, nb, N // S, pt, ins, ct, outs, L, N)
+    return dict(cipher=cfg["cipher"], records=N, len=L, states=S, recs_per_state=N // S,
+                in_stride=ins, out_stride=outs,
+                pt_sha256=hashlib.sha256(pt.reshape(N, ins)[:, :L].tobytes()).hexdigest(),
+                sealed_sha256=hashlib.sha256(ct.reshape(N, outs)[:, :L + 16].tobytes()).hexdigest())
+
+
+def ref_digest(o, cfg):
+    """C2's sealed digest through the reference's own CipherState API
+    (oracle/_ref, built from /root/reference), one call per record."""
+    ref = RefLib()
+    N, L = cfg["records"], cfg["len"]
+    ins = stride(L)
+    key = o.fill(SEED_KEY, 32, 0)
+    pt = o.fill(SEED_PT, N * ins, 0)
+    h = hashlib.sha256()
+    for i in range(N):
+        h.update(ref.encrypt(cfg["cipher"], key, i, pt[i * ins:i * ins + L]))
+    return h.hexdigest()
+
+
+def main():
+    o = Oracle()
+    out = {"generator": "tests/golden/gen_config_digests.py (CPU oracle)", "configs": {}}
+    for name, cfg in CONFIGS.items():
+        t = time.time()
+        out["configs"][name] = digests(o, name, cfg)
+        print(name, f"{time.time() - t:.1f}s", out["configs"][name]["sealed_sha256"][:16])
+    if os.path.exists(REF_SO):
+        d = ref_digest(o, CONFIGS["c2"])
+        assert d == out["configs"]["c2"]["sealed_sha256"], "oracle != reference on C2"
+        out["configs"]["c2"]["reference_checked"] = True
+        print("c2 reference build agrees")
+    with open(os.path.join(ROOT, "tests", "golden", "config_digests.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
