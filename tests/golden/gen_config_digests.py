@@ -65,6 +65,33 @@ def ref_digest(o, cfg):
     return h.hexdigest()
 
 
+def c5_digest(o):
+    """C5 at N = 1 (bench.py run_mixed, rank 0): 128 Ki records of 64 B-16 KiB
+    over 512 states, ChaChaPoly for even states and AES-GCM for odd, record j
+    at slot offset off[j] with nonce j % rps.  Sealed through the reference
+    build (its AES is ~30x faster than the bit-serial oracle here); every
+    64th record is re-sealed by the oracle as a cross-check."""
+    sys.path.insert(0, ROOT)
+    from bench import CONFIGS as BC, mixed_layout
+    R, S = BC["c5"]["records"], BC["c5"]["states"]
+    lay = mixed_layout(R, S, 0)
+    pt = o.fill(SEED_PT, lay["total"], 0)
+    ref = RefLib()
+    keys = [o.fill(SEED_KEY, 32, 4 * s) for s in range(S)]
+    hp, hs = hashlib.sha256(), hashlib.sha256()
+    for j in range(R):
+        s, off, L, n = int(lay["st_global"][j]), int(lay["off"][j]), int(lay["lens"][j]), int(lay["nonce"][j])
+        cipher = CHACHA if s % 2 == 0 else AES
+        p = pt[off:off + L]
+        c = ref.encrypt(cipher, keys[s], n, p)
+        if j % 64 == 0:
+            assert c == o.encrypt(cipher, keys[s], n, p), j
+        hp.update(p)
+        hs.update(c)
+    return dict(records=R, states=S, lens_sum=int(lay["lens"].sum()), total=lay["total"],
+                pt_sha256=hp.hexdigest(), sealed_sha256=hs.hexdigest(), reference_checked=True)
+
+
 def main():
     o = Oracle()
     out = {"generator": "tests/golden/gen_config_digests.py (CPU oracle)", "configs": {}}
@@ -77,6 +104,9 @@ def main():
         assert d == out["configs"]["c2"]["sealed_sha256"], "oracle != reference on C2"
         out["configs"]["c2"]["reference_checked"] = True
         print("c2 reference build agrees")
+        t = time.time()
+        out["configs"]["c5"] = c5_digest(o)
+        print("c5", f"{time.time() - t:.1f}s", out["configs"]["c5"]["sealed_sha256"][:16])
     with open(os.path.join(ROOT, "tests", "golden", "config_digests.json"), "w") as f:
         json.dump(out, f, indent=1)
 

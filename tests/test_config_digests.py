@@ -75,3 +75,67 @@ def test_full_config_digest_on_gpu(name):
     assert int(st.max().item()) == 0
     opened = back.view(N, ins)[:, :L].contiguous().cpu().numpy()
     assert hashlib.sha256(opened.tobytes()).hexdigest() == c["pt_sha256"], name
+
+
+@pytest.mark.gpu
+def test_full_c5_digest_on_gpu():
+    """C5 at N = 1 (bench.py run_mixed, rank 0): the mixed ChaChaPoly/AES-GCM
+    ragged batch, 128 Ki records of 64 B-16 KiB over 512 states, sealed with
+    the FAST ragged kernels; every record's ct || tag, in record order, hashes
+    to the digest of the reference build, and the open accepts them all and
+    restores every plaintext."""
+    import torch
+
+    import noise_aead as A
+    from bench import CHACHA, AES, CONFIGS as BC, mixed_layout
+    A.lib()
+    c = _golden()["c5"]
+    R, S = BC["c5"]["records"], BC["c5"]["states"]
+    assert (R, S) == (c["records"], c["states"])
+    lay = mixed_layout(R, S, 0)
+    assert lay["total"] == c["total"] and int(lay["lens"].sum()) == c["lens_sum"]
+    sp = torch.cuda.current_stream().cuda_stream
+    rec_dt = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "<u8"),
+                       ("ad_off", "<u8"), ("len", "<u4"), ("ad_len", "<u4")])
+    pt = torch.empty(lay["total"], dtype=torch.uint8, device="cuda")
+    assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), SEED_PT, 0, sp) == 0
+    ct = torch.zeros_like(pt)
+    back = torch.zeros_like(pt)
+    groups = []
+    for cipher, parity in ((CHACHA, 0), (AES, 1)):
+        states = [s for s in range(S) if s % 2 == parity]
+        cb = A.dev_ctx_bytes(cipher)
+        raw = torch.empty(len(states) * 32, dtype=torch.uint8, device="cuda")
+        for i, s in enumerate(states):
+            assert A.dev_fill_splitmix(raw[32 * i:].data_ptr(), 32, SEED_KEY, 4 * s, sp) == 0
+        ctx = torch.empty(len(states) * cb, dtype=torch.uint8, device="cuda")
+        assert A.dev_prepare(cipher, raw.data_ptr(), len(states), ctx.data_ptr(), sp) == 0
+        slot_of = {s: i for i, s in enumerate(states)}
+        idx = np.nonzero((lay["st_global"] % 2) == parity)[0]
+        recs = np.zeros(len(idx), dtype=rec_dt)
+        recs["in_off"] = lay["off"][idx]
+        recs["out_off"] = lay["off"][idx]
+        recs["nonce"] = lay["nonce"][idx]
+        recs["ctx_off"] = np.array([slot_of[s] for s in lay["st_local"][idx]], dtype=np.uint64) * cb
+        recs["len"] = lay["lens"][idx]
+        d_recs = torch.from_numpy(recs.view(np.uint8)).to("cuda")
+        st = torch.full((len(idx),), 9, dtype=torch.uint8, device="cuda")
+        groups.append((cipher, ctx, d_recs, len(idx), st))
+    for open_, src, dst in ((False, pt, ct), (True, ct, back)):
+        for cipher, ctx, d_recs, n, st in groups:
+            rc = A.dev_ragged(open_, cipher, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
+                              inp=src.data_ptr(), out=dst.data_ptr(), n_records=n,
+                              status=st.data_ptr() if open_ else 0, flags=A.FLAG_FAST, stream=sp)
+            assert rc == 0
+    torch.cuda.synchronize()
+    for g in groups:
+        assert int(g[4].max().item()) == 0
+    ct_h, back_h, pt_h = ct.cpu().numpy(), back.cpu().numpy(), pt.cpu().numpy()
+    hs, hb, hp = hashlib.sha256(), hashlib.sha256(), hashlib.sha256()
+    for off, L in zip(lay["off"].tolist(), lay["lens"].tolist()):
+        hs.update(ct_h[off:off + L + 16])
+        hb.update(back_h[off:off + L])
+        hp.update(pt_h[off:off + L])
+    assert hp.hexdigest() == c["pt_sha256"]
+    assert hs.hexdigest() == c["sealed_sha256"]
+    assert hb.hexdigest() == c["pt_sha256"]
