@@ -186,10 +186,13 @@ def _cpu_baseline(cfg, budget_cpu_s):
             "ok": r["ok"]}
 
 
-def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length):
-    """The seal kernel the library dispatches for this uniform job
-    (aead_api.hip run_uniform), as rocprofv3 names it."""
+def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length, duplex=False):
+    """The kernel the library dispatches for this uniform job's seal
+    (aead_api.hip run_uniform) or, duplex, for the whole step (run_duplex), as
+    rocprofv3 names it."""
     fast = in_stride % 16 == 0 and out_stride % 16 == 0 and in_stride >= (max(length, 1) + 63) // 64 * 64
+    if duplex and cipher == CHACHA and fast and lanes in (4, 8):
+        return f"chachapoly_duplex_staged<{lanes}, {'true' if rps % (64 // lanes) == 0 else 'false'}>"
     if cipher == AES:
         return "gcm_staged<false>" if fast and rps % 256 == 0 else "gcm_uniform<false>"
     if fast and lanes >= 4:
@@ -242,6 +245,12 @@ def main():
     ap.add_argument("--no-xfer", action="store_true",
                     help="skip the N>1 scatter/seal/gather leg (RCCL, SURVEY.md 8e)")
     ap.add_argument("--xfer-reps", type=int, default=5)
+    ap.add_argument("--mode", default="duplex", choices=("duplex", "separate"),
+                    help="duplex: each step seals one set and opens another in ONE launch "
+                         "(noise_aead_dev_duplex_uniform); separate: a seal launch then an open launch")
+    ap.add_argument("--events", default="ends", choices=("ends", "step"),
+                    help="ends: HIP events only around the timed region (per-launch time = "
+                         "its interval / launches); step: events at every launch boundary")
     ap.add_argument("--streams", type=int, default=1, choices=(1, 2),
                     help="C2-C4/perf: 2 = consecutive steps alternate between two streams")
     ap.add_argument("--c5-streams", type=int, default=2, choices=(1, 2),
@@ -326,30 +335,74 @@ def main():
                              recs_per_state=sh["rps"], status=st.data_ptr(), lanes=lanes,
                              stream=stream, **ad_kw)
 
-    # --streams 2: consecutive steps (independent batch sets) alternate between
-    # two streams, so step s+1's seal can start on CUs that step s's open is
-    # leaving (a server pipelining independent batches).  Each step's seal ->
-    # open stays ordered on its own stream; set b is reused only every
-    # `sets` steps, on the same stream.
-    streams = [stream] + ([torch.cuda.Stream(dev)] if args.streams == 2 else [])
+    # Each step seals set b = s % sets and opens set (s - LAG) % sets, sealed LAG
+    # steps earlier: the ciphertext an open reads was written two full steps
+    # (> 700 MB of traffic) before, so it comes from HBM, not from the 256 MiB
+    # Infinity Cache.  Every set is sealed once before timing, so every open
+    # has ciphertext; a set's ciphertext is the same at every seal.
+    lag = 2 if args.sets >= 3 else 0
+    duplex = args.mode == "duplex"
 
+    def jobs(b, bo, stream):
+        pt, ct, _, _ = sets[b]
+        _, cto, back, st = sets[bo]
+        common = dict(ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(), length=L, n_records=N,
+                      recs_per_state=sh["rps"], lanes=lanes, **ad_kw)
+        sj = A.uniform_job(inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
+                           out_stride=out_stride, **common)
+        oj = A.uniform_job(inp=cto.data_ptr(), out=back.data_ptr(), in_stride=out_stride,
+                           out_stride=in_stride, status=st.data_ptr(), **common)
+        return sj, oj
+
+    def step_duplex(b, bo, stream=sp):
+        sj, oj = jobs(b, bo, stream)
+        return A.dev_duplex(cipher, sj, oj, stream)
+
+    # --streams 2 (separate mode): consecutive steps (independent batch sets)
+    # alternate between two streams, so step s+1's seal can start on CUs that
+    # step s's open is leaving.  Set b is reused only every `sets` steps.
+    streams = [stream] + ([torch.cuda.Stream(dev)] if args.streams == 2 and not duplex else [])
+
+    for b in range(args.sets):
+        assert seal(b) == 0
     for w in range(args.warmup):
-        assert seal(w % args.sets) == 0
-        assert open_(w % args.sets) == 0
+        b, bo = w % args.sets, (w - lag) % args.sets
+        if duplex:
+            assert step_duplex(b, bo) == 0
+        else:
+            assert seal(b) == 0
+            assert open_(bo) == 0
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    per_step = args.events == "step"
+    if duplex or not per_step:  # launch boundaries (duplex) or just the region's ends
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    else:
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+               torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    if duplex or not per_step:
+        ev[0].record(stream)
     for s in range(args.steps):
-        b = s % args.sets
+        b, bo = s % args.sets, (s - lag) % args.sets
+        if duplex or not per_step:
+            if duplex:
+                rc = step_duplex(b, bo)
+            else:
+                st_ = streams[s % len(streams)].cuda_stream
+                rc = seal(b, stream=st_) or open_(bo, stream=st_)
+            if per_step or s == args.steps - 1:
+                ev[s + 1].record(stream)
+            if rc:
+                raise RuntimeError(f"launch failed {rc:#x}")
+            continue
         st_ = streams[s % len(streams)]
         ev[s][0].record(st_)
         rc1 = seal(b, stream=st_.cuda_stream)
         ev[s][1].record(st_)
-        rc2 = open_(b, stream=st_.cuda_stream)
+        rc2 = open_(bo, stream=st_.cuda_stream)
         ev[s][2].record(st_)
         if rc1 or rc2:
             raise RuntimeError(f"launch failed {rc1:#x} {rc2:#x}")
@@ -361,11 +414,14 @@ def main():
         elapsed = float(t.item())
         dist.barrier()
 
-    seal_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-    open_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
-    if len(streams) > 1:
-        # overlapped launches stretch each other's events: the per-launch
-        # times of the roofline come from a serial, untimed pass instead
+    if duplex or not per_step:
+        # average launch interval over the timed region, gaps included
+        launch_ms = ev[0].elapsed_time(ev[args.steps]) / args.steps / (1 if duplex else 2)
+    else:
+        seal_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+        open_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
+    if duplex or not per_step or len(streams) > 1:
+        # per-direction launch times (separate kernels) from a serial, untimed pass
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         reps = 5
         e[0].record(stream)
@@ -373,7 +429,7 @@ def main():
             seal(r % args.sets)
         e[1].record(stream)
         for r in range(reps):
-            open_(r % args.sets)
+            open_((r - lag) % args.sets)
         e[2].record(stream)
         torch.cuda.synchronize(dev)
         seal_ms = e[0].elapsed_time(e[1]) / reps
@@ -381,7 +437,7 @@ def main():
 
     ok = True
     if args.verify:
-        for b in range(min(args.sets, args.steps)):
+        for b in range(args.sets):
             pt, _, back, st = sets[b]
             ok &= bool((st == 0).all().item())
             v = pt.view(N, in_stride)[:, :L]
@@ -390,8 +446,16 @@ def main():
     payload_step = 2.0 * N * L * world                         # both directions, all ranks
     value = payload_step * args.steps / elapsed / GIB
     alg_seal = N * (2 * L + 16 + AD) + len(sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
-    achieved = alg_seal / (seal_ms * 1e-3) / 1e9
-    kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L)
+    kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L, duplex)
+    if kname.startswith("chachapoly_duplex"):
+        # the one launch of a step: one seal + one open of N records each
+        alg_launch, launch_ms_ = 2 * alg_seal, launch_ms
+    elif not duplex and not per_step:
+        # seal and open alternate: the mean interval per launch, gaps included
+        alg_launch, launch_ms_ = alg_seal, launch_ms
+    else:
+        alg_launch, launch_ms_ = alg_seal, seal_ms
+    achieved = alg_launch / (launch_ms_ * 1e-3) / 1e9
     pmc = load_pmc(args.config, kname, 1.0 / world if cfg.get("strong") else 1.0)
     traffic = pmc.get("hbm_bytes_per_launch")
     result = {
@@ -415,13 +479,14 @@ def main():
                    "record_len": L, "states_per_gpu": S, "lanes_per_record": lanes,
                    "in_stride": in_stride, "out_stride": out_stride,
                    "payload_bytes_per_step": int(payload_step), "parallelism": f"records x{world}",
-                   "streams": len(streams)},
+                   "streams": len(streams), "mode": args.mode, "events": args.events,
+                   "open_reads_set_sealed_steps_before": lag},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": kname,
-                     "algorithmic_bytes_per_launch": alg_seal,
-                     "avg_launch_ms": round(seal_ms, 5),
-                     "issue_bound": issue_bound(pmc, seal_ms)},
+                     "algorithmic_bytes_per_launch": alg_launch,
+                     "avg_launch_ms": round(launch_ms_, 5),
+                     "issue_bound": issue_bound(pmc, launch_ms_)},
         "seal_gibs": round(N * L * world / (seal_ms * 1e-3) / GIB, 2),
         "open_gibs": round(N * L * world / (open_ms * 1e-3) / GIB, 2),
         "open_roofline_frac": round(alg_seal / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

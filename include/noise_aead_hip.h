@@ -206,6 +206,18 @@ typedef struct NoiseAeadUniform {
 int noise_aead_dev_seal_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream);
 int noise_aead_dev_open_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream);
 
+/* Duplex: seal_job and open_job in one launch — an echo server's two
+ * directions (echo-server.c:377-407 opens what it receives and seals what it
+ * sends) or a pipeline sealing one batch while opening an earlier one.  The
+ * result is exactly noise_aead_dev_seal_uniform(seal_job) followed by
+ * noise_aead_dev_open_uniform(open_job); the jobs must be independent (no
+ * record memory of one job may overlap output memory of the other:
+ * NOISE_ERROR_INVALID_PARAM).  Either job may have n_records == 0.  When the
+ * two jobs cannot share a kernel (AESGCM, unaligned layouts, different lane
+ * counts) the library issues the two launches on `stream` instead. */
+int noise_aead_dev_duplex_uniform(int cipher_id, const NoiseAeadUniform *seal_job,
+                                  const NoiseAeadUniform *open_job, void *stream);
+
 /* Ragged batch: one descriptor per record.  The key context of a record is
  * at ctx_base + ctx_off (ctx_base may be NULL with absolute ctx_off). */
 typedef struct NoiseAeadRecord {

@@ -188,8 +188,10 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
         const bool ukey = k >= 4 && job->recs_per_state % (64u / (uint32_t)k) == 0;
         KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open), ukey);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
-        /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC) */
-        a.balance = (uint64_t)job->n_records * (uint32_t)k <= 4096ull * 64;
+        /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC): open
+           balances its waves' progress (profiles/r01_prio_ab.jsonl); in the
+           seal it measured neutral (profiles/r02/timeline_c2_seal_open_duplex.log) */
+        a.balance = open && (uint64_t)job->n_records * (uint32_t)k <= 4096ull * 64;
         return launch(fn, job->n_records, k, a, s);
     }
     if (cipher_id == NOISE_CIPHER_AESGCM) {
@@ -209,6 +211,57 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
                       GCM_LANES, a, s);
     }
     return NOISE_ERROR_UNKNOWN_ID;
+}
+
+/* Byte span [lo, hi) a uniform job's input (or output) records occupy. */
+void job_span(const NoiseAeadUniform *j, bool out, bool open, uint64_t &lo, uint64_t &hi)
+{
+    const uint64_t base = (uint64_t)(uintptr_t)(out ? (const void *)j->out : (const void *)j->in);
+    const uint64_t stride = out ? j->out_stride : j->in_stride;
+    const uint64_t rec = (uint64_t)j->len + ((out != open) ? 16u : 0u); /* CT || tag side */
+    lo = base;
+    hi = j->n_records ? base + (uint64_t)(j->n_records - 1) * stride + rec : base;
+}
+
+bool spans_overlap(const NoiseAeadUniform *a, bool a_out, bool a_open,
+                   const NoiseAeadUniform *b, bool b_out, bool b_open)
+{
+    uint64_t al, ah, bl, bh;
+    job_span(a, a_out, a_open, al, ah);
+    job_span(b, b_out, b_open, bl, bh);
+    return al < bh && bl < ah;
+}
+
+int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform *oj, void *stream)
+{
+    int rc = check_uniform(sj);
+    if (!rc) rc = check_uniform(oj);
+    if (rc) return rc;
+    /* independent jobs: neither writes what the other reads or writes */
+    if (sj->n_records && oj->n_records &&
+        (spans_overlap(sj, true, false, oj, false, true) || spans_overlap(sj, true, false, oj, true, true) ||
+         spans_overlap(oj, true, true, sj, false, false)))
+        return NOISE_ERROR_INVALID_PARAM;
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY && sj->n_records && oj->n_records) {
+        const int ks = sj->lanes_per_record ? (int)sj->lanes_per_record : auto_lanes(sj->n_records, 0);
+        const int ko = oj->lanes_per_record ? (int)oj->lanes_per_record : auto_lanes(oj->n_records, 0);
+        const bool us = ks >= 4 && sj->recs_per_state % (64u / (uint32_t)ks) == 0;
+        const bool uo = ko >= 4 && oj->recs_per_state % (64u / (uint32_t)ko) == 0;
+        if (ks == ko && (ks == 4 || ks == 8) && us == uo && uniform_fast(sj, false) &&
+            uniform_fast(oj, true)) {
+            UniformArgs a = to_args(sj), b = to_args(oj);
+            const uint32_t sb = (uint32_t)(((uint64_t)sj->n_records * ks + 255) / 256);
+            const uint32_t ob = (uint32_t)(((uint64_t)oj->n_records * ko + 255) / 256);
+            void (*fn)(UniformArgs, UniformArgs, uint32_t, uint32_t);
+            if (ks == 4) fn = us ? chachapoly_duplex_staged<4, true> : chachapoly_duplex_staged<4, false>;
+            else fn = us ? chachapoly_duplex_staged<8, true> : chachapoly_duplex_staged<8, false>;
+            hipLaunchKernelGGL(fn, dim3(sb + ob), dim3(256), 0, (hipStream_t)stream, a, b, sb, ob);
+            return hip_rc(hipGetLastError());
+        }
+    }
+    rc = run_uniform(cipher_id, sj, stream, false);
+    if (!rc) rc = run_uniform(cipher_id, oj, stream, true);
+    return rc;
 }
 
 int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool open)
@@ -319,6 +372,12 @@ int noise_aead_dev_seal_uniform(int cipher_id, const NoiseAeadUniform *job, void
 int noise_aead_dev_open_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream)
 {
     return run_uniform(cipher_id, job, stream, true);
+}
+
+int noise_aead_dev_duplex_uniform(int cipher_id, const NoiseAeadUniform *seal_job,
+                                  const NoiseAeadUniform *open_job, void *stream)
+{
+    return run_duplex(cipher_id, seal_job, open_job, stream);
 }
 
 int noise_aead_dev_seal_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream)

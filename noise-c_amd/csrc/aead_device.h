@@ -50,6 +50,76 @@ NA_DEV void chacha20_block(const uint32_t key[8], uint32_t ctr_lo, uint32_t ctr_
     x[12] += ctr_lo; x[13] += ctr_hi; x[14] += iv_lo; x[15] += iv_hi;
 }
 
+/* The block-independent part of the first column round.  Of the four column
+   quarter-rounds of round 1 only QR(0,4,8,12) sees the block counter (word
+   12; word 13, the counter's high half, is 0 for every block of an AEAD
+   record, cipher-chachapoly.c:62-66): QR(1,5,9,13) depends on the key alone,
+   QR(2,6,10,14) and QR(3,7,11,15) on key and nonce.  A lane that runs several
+   blocks of one record computes them once (with a wave-uniform key the key-only
+   quarter-round is scalar work) and starts every block from them: 37 VALU
+   instructions of ~1000 per block fewer. */
+struct ChaPre {
+    uint32_t a0;           /* x0 + x4, the first step of QR(0,4,8,12) */
+    uint32_t c1[4];        /* x1, x5, x9, x13 after QR(1,5,9,13) */
+    uint32_t c2[4];        /* x2, x6, x10, x14 after QR(2,6,10,14) */
+    uint32_t c3[4];        /* x3, x7, x11, x15 after QR(3,7,11,15) */
+};
+
+NA_DEV void chacha_pre(const uint32_t key[8], uint32_t iv_lo, uint32_t iv_hi, ChaPre &p)
+{
+    uint32_t a, b, c, d;
+    p.a0 = 0x61707865u + key[0];
+    a = 0x3320646eu; b = key[1]; c = key[5]; d = 0u;
+    NA_QR(a, b, c, d);
+    p.c1[0] = a; p.c1[1] = b; p.c1[2] = c; p.c1[3] = d;
+    a = 0x79622d32u; b = key[2]; c = key[6]; d = iv_lo;
+    NA_QR(a, b, c, d);
+    p.c2[0] = a; p.c2[1] = b; p.c2[2] = c; p.c2[3] = d;
+    a = 0x6b206574u; b = key[3]; c = key[7]; d = iv_hi;
+    NA_QR(a, b, c, d);
+    p.c3[0] = a; p.c3[1] = b; p.c3[2] = c; p.c3[3] = d;
+}
+
+/* NA_CHACHA_PRE=0 builds the plain block function (A/B measurements). */
+#ifndef NA_CHACHA_PRE
+#define NA_CHACHA_PRE 1
+#endif
+
+/* chacha20_block(key, ctr, 0, iv_lo, iv_hi, x) from the precomputed columns. */
+NA_DEV void chacha20_block_pre(const uint32_t key[8], const ChaPre &p, uint32_t ctr,
+                               uint32_t iv_lo, uint32_t iv_hi, uint32_t x[16])
+{
+#if !NA_CHACHA_PRE
+    (void)p;
+    chacha20_block(key, ctr, 0u, iv_lo, iv_hi, x);
+    return;
+#endif
+    /* rest of round 1, column 0: a = x0 + x4 is p.a0 */
+    uint32_t a = p.a0, b = key[0], c = key[4], d = ctr;
+    d ^= a; d = rotl(d, 16);
+    c += d; b ^= c; b = rotl(b, 12);
+    a += b; d ^= a; d = rotl(d, 8);
+    c += d; b ^= c; b = rotl(b, 7);
+    x[0] = a; x[4] = b; x[8] = c; x[12] = d;
+    x[1] = p.c1[0]; x[5] = p.c1[1]; x[9] = p.c1[2]; x[13] = p.c1[3];
+    x[2] = p.c2[0]; x[6] = p.c2[1]; x[10] = p.c2[2]; x[14] = p.c2[3];
+    x[3] = p.c3[0]; x[7] = p.c3[1]; x[11] = p.c3[2]; x[15] = p.c3[3];
+    /* round 1's diagonal half, then double rounds 2..10 */
+    NA_QR(x[0], x[5], x[10], x[15]); NA_QR(x[1], x[6], x[11], x[12]);
+    NA_QR(x[2], x[7], x[8], x[13]);  NA_QR(x[3], x[4], x[9], x[14]);
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        NA_QR(x[0], x[4], x[8], x[12]);  NA_QR(x[1], x[5], x[9], x[13]);
+        NA_QR(x[2], x[6], x[10], x[14]); NA_QR(x[3], x[7], x[11], x[15]);
+        NA_QR(x[0], x[5], x[10], x[15]); NA_QR(x[1], x[6], x[11], x[12]);
+        NA_QR(x[2], x[7], x[8], x[13]);  NA_QR(x[3], x[4], x[9], x[14]);
+    }
+    x[0] += 0x61707865u; x[1] += 0x3320646eu; x[2] += 0x79622d32u; x[3] += 0x6b206574u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[4 + i] += key[i];
+    x[12] += ctr; x[14] += iv_lo; x[15] += iv_hi;
+}
+
 /* ------------------------------------------------------------- Poly1305 */
 
 constexpr uint32_t M26 = 0x3ffffffu;
@@ -217,36 +287,36 @@ NA_DEV R32 r32_from_key(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3)
     return r;
 }
 
+/* 32x32 -> 64 multiply-add: one v_mad_u64_u32 */
+NA_DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
+
 NA_DEV void p32_block(P32 &h, const R32 &r, uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3)
 {
-    uint64_t t = (uint64_t)h.h0 + m0;
-    const uint32_t a0 = (uint32_t)t;
-    t = (uint64_t)h.h1 + m1 + (t >> 32);
-    const uint32_t a1 = (uint32_t)t;
-    t = (uint64_t)h.h2 + m2 + (t >> 32);
-    const uint32_t a2 = (uint32_t)t;
-    t = (uint64_t)h.h3 + m3 + (t >> 32);
-    const uint32_t a3 = (uint32_t)t;
-    const uint32_t a4 = h.h4 + (uint32_t)(t >> 32) + 1u; /* the 2^128 pad bit */
-    uint64_t d0 = (uint64_t)a0 * r.r0 + (uint64_t)a1 * r.s3 + (uint64_t)a2 * r.s2 +
-                  (uint64_t)a3 * r.s1;
-    uint64_t d1 = (d0 >> 32) + (uint64_t)a0 * r.r1 + (uint64_t)a1 * r.r0 +
-                  (uint64_t)a2 * r.s3 + (uint64_t)a3 * r.s2 + (uint64_t)a4 * r.s1;
-    uint64_t d2 = (d1 >> 32) + (uint64_t)a0 * r.r2 + (uint64_t)a1 * r.r1 +
-                  (uint64_t)a2 * r.r0 + (uint64_t)a3 * r.s3 + (uint64_t)a4 * r.s2;
-    uint64_t d3 = (d2 >> 32) + (uint64_t)a0 * r.r3 + (uint64_t)a1 * r.r2 +
-                  (uint64_t)a2 * r.r1 + (uint64_t)a3 * r.r0 + (uint64_t)a4 * r.s3;
-    const uint32_t h4 = a4 * r.r0 + (uint32_t)(d3 >> 32);   /* < 2^31.4 */
-    const uint32_t c = (h4 & ~3u) + (h4 >> 2);                /* 5 * (h4 >> 2) */
-    t = (uint64_t)(uint32_t)d0 + c;
-    h.h0 = (uint32_t)t;
-    t = (uint64_t)(uint32_t)d1 + (t >> 32);
-    h.h1 = (uint32_t)t;
-    t = (uint64_t)(uint32_t)d2 + (t >> 32);
-    h.h2 = (uint32_t)t;
-    t = (uint64_t)(uint32_t)d3 + (t >> 32);
-    h.h3 = (uint32_t)t;
-    h.h4 = (h4 & 3u) + (uint32_t)(t >> 32);
+    /* h + m + 2^128 as a 32-bit carry chain (v_add_co / v_addc_co; written
+       with 64-bit adds hipcc builds each step from v_mov + v_lshl_add_u64) */
+    unsigned int c;
+    const uint32_t a0 = __builtin_addc(h.h0, m0, 0u, &c);
+    const uint32_t a1 = __builtin_addc(h.h1, m1, c, &c);
+    const uint32_t a2 = __builtin_addc(h.h2, m2, c, &c);
+    const uint32_t a3 = __builtin_addc(h.h3, m3, c, &c);
+    const uint32_t a4 = __builtin_addc(h.h4, 1u, c, &c); /* the 2^128 pad bit */
+    /* columns: each chain of v_mad_u64_u32 starts from the previous column's
+       high word */
+    uint64_t d0 = mad64(a3, r.s1, mad64(a2, r.s2, mad64(a1, r.s3, (uint64_t)a0 * r.r0)));
+    uint64_t d1 = mad64(a4, r.s1, mad64(a3, r.s2, mad64(a2, r.s3, mad64(a1, r.r0,
+                  mad64(a0, r.r1, d0 >> 32)))));
+    uint64_t d2 = mad64(a4, r.s2, mad64(a3, r.s3, mad64(a2, r.r0, mad64(a1, r.r1,
+                  mad64(a0, r.r2, d1 >> 32)))));
+    uint64_t d3 = mad64(a4, r.s3, mad64(a3, r.r0, mad64(a2, r.r1, mad64(a1, r.r2,
+                  mad64(a0, r.r3, d2 >> 32)))));
+    const uint32_t h4 = a4 * r.r0 + (uint32_t)(d3 >> 32); /* a4 <= 8: < 2^31.4 */
+    const uint32_t q = h4 >> 2;
+    const uint32_t f = (q << 2) + q;                               /* 5 * (h4 >> 2) */
+    h.h0 = __builtin_addc((uint32_t)d0, f, 0u, &c);
+    h.h1 = __builtin_addc((uint32_t)d1, 0u, c, &c);
+    h.h2 = __builtin_addc((uint32_t)d2, 0u, c, &c);
+    h.h3 = __builtin_addc((uint32_t)d3, 0u, c, &c);
+    h.h4 = (h4 & 3u) + c;
 }
 
 /* radix 2^32 -> five 26-bit limbs (for the rare generic multiplies) */

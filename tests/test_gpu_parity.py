@@ -179,6 +179,71 @@ def test_uniform_staged_kernels(aead, gpu, oracle, cipher):
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L]), f"len={L} rec={i}"
 
 
+@pytest.mark.parametrize("cipher,lanes,layout", [(CHACHA, 4, "fast"), (CHACHA, 8, "fast"),
+                                                 (CHACHA, 4, "packed"), (AES, 0, "fast")])
+def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout):
+    """noise_aead_dev_duplex_uniform: seal job A and open job B (other keys,
+    nonces, length, record count; some records tampered) in one call must
+    equal the two separate calls — i.e. the oracle — byte for byte.  ChaCha
+    FAST layouts run the one-launch duplex kernel, the others two launches."""
+    torch = _torch()
+    rng = np.random.default_rng(3131 + lanes + (cipher & 3) + len(layout))
+    for (La, na, rpsa), (Lb, nb_, rpsb) in [((1400, 700, 350), (1400, 300, 100)),
+                                           ((100, 64, 16), (1401, 513, 513)),
+                                           ((0, 33, 16), (65, 1000, 16)), ((4096, 5, 5), (17, 0, 1))]:
+        def strides(L):
+            if layout == "packed":
+                return L, L + 16
+            return (max(L, 1) + 63) // 64 * 64, (L + 16 + 63) // 64 * 64
+        ia, oa = strides(La)
+        ib, ob = strides(Lb)
+        Sa, Sb = (na + rpsa - 1) // rpsa, max(1, (nb_ + rpsb - 1) // rpsb)
+        ka = rng.integers(0, 256, (Sa, 32), dtype=np.uint8)
+        kb = rng.integers(0, 256, (Sb, 32), dtype=np.uint8)
+        nba = rng.integers(0, 2**62, Sa, dtype=np.uint64)
+        nbb = rng.integers(0, 2**62, Sb, dtype=np.uint64)
+        pta = rng.integers(0, 256, na * ia + 64, dtype=np.uint8)
+        ptb = rng.integers(0, 256, max(1, nb_) * ib + 64, dtype=np.uint8)
+        exp_a = oracle_seal_records(oracle, cipher, ka, nba, rpsa, pta, ia, La, na, oa)
+        ctb = oracle_seal_records(oracle, cipher, kb, nbb, rpsb, ptb, ib, Lb, nb_, ob)
+        bad = sorted(set(int(x) for x in rng.integers(0, max(1, nb_), 4))) if nb_ else []
+        for b in bad:
+            ctb[b * ob + int(rng.integers(0, Lb + 16))] ^= 0x10
+        ctxa, _k1 = prepare(aead, cipher, ka)
+        ctxb, _k2 = prepare(aead, cipher, kb)
+        d_nba, d_nbb = dev(nba.view(np.int64)), dev(nbb.view(np.int64))
+        d_pta, d_ctb = dev(pta), dev(ctb)
+        d_outa = torch.full((na * oa + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        d_outb = torch.full((max(1, nb_) * ib + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+        d_st = torch.full((max(1, nb_),), 7, dtype=torch.uint8, device="cuda")
+        sj = aead.uniform_job(ctx=ctxa.data_ptr(), nonce_base=d_nba.data_ptr(), inp=d_pta.data_ptr(),
+                              out=d_outa.data_ptr(), in_stride=ia, out_stride=oa, length=La,
+                              n_records=na, recs_per_state=rpsa, lanes=lanes)
+        oj = aead.uniform_job(ctx=ctxb.data_ptr(), nonce_base=d_nbb.data_ptr(), inp=d_ctb.data_ptr(),
+                              out=d_outb.data_ptr(), in_stride=ob, out_stride=ib, length=Lb,
+                              n_records=nb_, recs_per_state=rpsb, status=d_st.data_ptr(),
+                              lanes=lanes)
+        assert aead.dev_duplex(cipher, sj, oj, stream()) == 0
+        sync()
+        got_a, back, st = d_outa.cpu().numpy(), d_outb.cpu().numpy(), d_st.cpu().numpy()
+        assert np.array_equal(got_a[:na * oa], exp_a[:na * oa]), f"duplex seal len={La}"
+        for i in range(nb_):
+            seg = back[i * ib: i * ib + Lb]
+            if i in bad:
+                assert st[i] == 1 and np.all(seg == 0x5A), f"duplex open len={Lb} rec={i}"
+            else:
+                assert st[i] == 0, f"duplex open len={Lb} rec={i}"
+                assert np.array_equal(seg, ptb[i * ib: i * ib + Lb]), f"len={Lb} rec={i}"
+    # overlapping jobs are refused (the seal's output is the open's input)
+    sj = aead.uniform_job(ctx=ctxa.data_ptr(), nonce_base=d_nba.data_ptr(), inp=d_pta.data_ptr(),
+                          out=d_outa.data_ptr(), in_stride=64, out_stride=64, length=10,
+                          n_records=4, recs_per_state=4)
+    oj = aead.uniform_job(ctx=ctxa.data_ptr(), nonce_base=d_nba.data_ptr(), inp=d_outa.data_ptr(),
+                          out=d_outb.data_ptr(), in_stride=64, out_stride=64, length=10,
+                          n_records=4, recs_per_state=4, status=d_st.data_ptr())
+    assert aead.dev_duplex(cipher, sj, oj, stream()) == 0x450B
+
+
 @pytest.mark.parametrize("cipher,lanes", [(CHACHA, 1), (CHACHA, 4), (CHACHA, 8), (CHACHA, 32),
                                           (CHACHA, 64), (AES, 0)])
 @pytest.mark.parametrize("rps", [4, 16])
