@@ -57,7 +57,9 @@ NA_DEV void chacha20_block(const uint32_t key[8], uint32_t ctr_lo, uint32_t ctr_
    QR(2,6,10,14) and QR(3,7,11,15) on key and nonce.  A lane that runs several
    blocks of one record computes them once (with a wave-uniform key the key-only
    quarter-round is scalar work) and starts every block from them: 37 VALU
-   instructions of ~1000 per block fewer. */
+   instructions of ~1000 per block fewer.  (hipcc hoists the same work out of
+   a lane's block loop by itself — profiles/r02/ — so this mostly states the
+   structure and keeps it independent of that optimisation.) */
 struct ChaPre {
     uint32_t a0;           /* x0 + x4, the first step of QR(0,4,8,12) */
     uint32_t c1[4];        /* x1, x5, x9, x13 after QR(1,5,9,13) */
@@ -80,20 +82,10 @@ NA_DEV void chacha_pre(const uint32_t key[8], uint32_t iv_lo, uint32_t iv_hi, Ch
     p.c3[0] = a; p.c3[1] = b; p.c3[2] = c; p.c3[3] = d;
 }
 
-/* NA_CHACHA_PRE=0 builds the plain block function (A/B measurements). */
-#ifndef NA_CHACHA_PRE
-#define NA_CHACHA_PRE 1
-#endif
-
 /* chacha20_block(key, ctr, 0, iv_lo, iv_hi, x) from the precomputed columns. */
 NA_DEV void chacha20_block_pre(const uint32_t key[8], const ChaPre &p, uint32_t ctr,
                                uint32_t iv_lo, uint32_t iv_hi, uint32_t x[16])
 {
-#if !NA_CHACHA_PRE
-    (void)p;
-    chacha20_block(key, ctr, 0u, iv_lo, iv_hi, x);
-    return;
-#endif
     /* rest of round 1, column 0: a = x0 + x4 is p.a0 */
     uint32_t a = p.a0, b = key[0], c = key[4], d = ctr;
     d ^= a; d = rotl(d, 16);

@@ -905,328 +905,6 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
 
 /* ------------------------------------------------- contiguous (K = 1, 2) */
 
-NA_DEV void p32_ad(P32 &acc, const R32 &r, const uint8_t *ad, uint32_t ad_len);
-NA_DEV void p32_unit(P32 &acc, const R32 &r, const uint32_t c[16], uint32_t nb);
-
-/* ------------------------------ contiguous runs, LDS-staged (K = 4 or 8)
- *
- * The uniform FAST kernels.  Lane k of a record's group owns the P =
- * ceil((J+1)/K) CONSECUTIVE ChaCha blocks v = kP .. kP+P-1, one per step
- * (block 0 = the Poly1305 key, block v >= 1 = data unit v-1).  Because a
- * lane's units are consecutive, its Poly1305 run is a plain Horner chain
- * h = (h + b) r with the clamped r, in radix 2^32 (p32_block: 20
- * v_mad_u64_u32, message words used as they are) — where the interleaved
- * decomposition (above) has to jump r^(4K-3) between a lane's units and so
- * needs the general radix-2^26 multiply for every block.  Lane 0 absorbs the
- * AD first, lane kl (the lane of block J) the length block; lane k < kl is
- * then scaled by r^A_k, A_k = the Poly blocks after its run, and the group
- * sums: sum_i b_i r^(n-i+1), the donna Horner value
- * (poly1305-donna-64.h:101-151).  ChaCha starts every block from the
- * first-round columns that do not depend on the counter (ChaPre).
- *
- * Global traffic goes through the same swizzled 4 KB LDS tile as the
- * interleaved kernels: at step m, owner L of the wave (record rec0 + L/K,
- * lane L%K) has unit (L%K)P + m - 1, so one coalesced wave-instruction moves
- * 16 runs of 64 B (each 128-B line's other half is the same owner's next
- * step, still in L2).
- */
-
-template <int K>
-struct RunPlan {
-    uint32_t J;  /* data units of 64 B */
-    uint32_t P;  /* blocks per lane = steps */
-    uint32_t M;  /* Poly1305 blocks of the ciphertext */
-    uint32_t kl; /* the lane holding block J (the last unit, the length block) */
-};
-
-template <int K>
-NA_DEV RunPlan<K> run_plan(uint32_t len)
-{
-    RunPlan<K> p;
-    p.J = (len + 63) / 64;
-    p.P = (p.J + K) / K; /* ceil((J + 1) / K) */
-    p.M = (len + 15) / 16;
-    p.kl = p.J / p.P;
-    return p;
-}
-
-/* Scale of lane k's partial sum: r^A_k, A_k = M + 5 - 4(k+1)P (the Poly
-   blocks after lane k's run, length block included) for k < kl; lanes from
-   kl on need none (kl's run ends with the length block, later lanes hold 0).
-   A_k = EX + (kl-1-k) EY, EX = A_(kl-1), EY = 4P: for a uniform batch both
-   exponents are wave-uniform, so one shared square chain serves X = r^EX and
-   Y = r^EY (scalar branches), then one lane-dependent multiply. */
-template <int K>
-NA_DEV Fe run_scale(const Fe &r, const RunPlan<K> &p, int k)
-{
-    const Fe one = Fe{1, 0, 0, 0, 0};
-    if (p.kl == 0) return one;
-    const uint32_t ey = 4 * p.P, ex = p.M + 5 - 4 * p.kl * p.P;
-    Fe R = r, X = one, Y = one;
-    bool hx = false, hy = false;
-    for (uint32_t bit = 0;; ++bit) {
-        if ((ex >> bit) & 1u) {
-            X = hx ? fe_mul(X, mk_mul(R)) : R;
-            hx = true;
-        }
-        if ((ey >> bit) & 1u) {
-            Y = hy ? fe_mul(Y, mk_mul(R)) : R;
-            hy = true;
-        }
-        if (((ex | ey) >> (bit + 1)) == 0) break;
-        R = fe_mul(R, mk_mul(R));
-    }
-    const int d = (int)p.kl - 1 - k; /* lane k < kl: X * Y^d */
-    Fe S = X;
-    if (p.kl >= 2) {
-        Fe Yp = Y;
-        for (int b = 0; (1 << b) < (int)p.kl; ++b) {
-            S = fe_mul(S, mk_mul((d >= 0 && ((d >> b) & 1)) ? Yp : one));
-            if ((2 << b) < (int)p.kl) Yp = fe_mul(Yp, mk_mul(Yp));
-        }
-    }
-    return k < (int)p.kl ? S : one;
-}
-
-/* Lane k's part of the tag: length block on lane kl, scale, group sum, + s. */
-template <int K>
-NA_DEV void run_close(P32 acc, const RunPlan<K> &p, int k, const R32 &r, const Fe &r26,
-                      uint64_t ad_len, uint64_t len, const uint32_t s[4], uint32_t tag[4])
-{
-    if (k == (int)p.kl)
-        p32_block(acc, r, (uint32_t)ad_len, (uint32_t)(ad_len >> 32), (uint32_t)len,
-                  (uint32_t)(len >> 32));
-    Fe h = p32_to_fe(acc);
-    h = fe_mul(h, mk_mul(run_scale<K>(r26, p, k)));
-    h = fe_group_sum<K>(h);
-    fe_finish(h, s, tag);
-}
-
-/* Poly key words from key-stream block 0, held by lane 0 of the group. */
-NA_DEV void run_poly_key(const uint32_t x[16], int gbase, R32 &r, Fe &r26, uint32_t s[4])
-{
-    uint32_t kw[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) kw[i] = (uint32_t)__shfl((int)x[i], gbase, 64);
-    r = r32_from_key(kw[0], kw[1], kw[2], kw[3]);
-    r26 = fe_clamp_r(kw[0], kw[1], kw[2], kw[3]);
-    s[0] = kw[4]; s[1] = kw[5]; s[2] = kw[6]; s[3] = kw[7];
-}
-
-template <int K>
-NA_DEV int run_unit(const WaveIO<K> &io, uint32_t P, uint32_t m)
-{
-    return io.kk * (int)P + (int)m - 1;
-}
-
-/* LDS-DMA of step m's units into tile t (owner units outside [0, J) read
-   unit 0: FAST slots are readable up to roundup64(max(len, 1))). */
-template <int K>
-NA_DEV void run_dma(const UniformArgs &a, const WaveIO<K> &io, const RunPlan<K> &p, uint32_t m,
-                    uint4 *t)
-{
-    const int u = run_unit<K>(io, p.P, m);
-    const uint32_t uu = (u >= 0 && (uint32_t)u < p.J) ? (uint32_t)u : 0u;
-    const uint32_t off = io.d16 + 64u * uu;
-    const uint32_t last = a.n_records - 1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        __builtin_amdgcn_global_load_lds(
-            (const void *)(a.in + (size_t)min(wave_rec(io, i), last) * a.in_stride + off),
-            (lds_void *)(t + 64 * i), 16, 0, 0);
-}
-
-/* Register-staged coalesced loads of step m (open's authentication pass). */
-template <int K>
-NA_DEV Quad run_load(const UniformArgs &a, const WaveIO<K> &io, const RunPlan<K> &p, uint32_t m)
-{
-    const int u = run_unit<K>(io, p.P, m);
-    const uint32_t uu = (u >= 0 && (uint32_t)u < p.J) ? (uint32_t)u : 0u;
-    const uint32_t off = io.c16 + 64u * uu;
-    const uint32_t last = a.n_records - 1;
-    Quad P;
-    P.a = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 0), last) * a.in_stride + off);
-    P.b = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 1), last) * a.in_stride + off);
-    P.c = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 2), last) * a.in_stride + off);
-    P.d = *(const uint4 *)(a.in + (size_t)min(wave_rec(io, 3), last) * a.in_stride + off);
-    return P;
-}
-
-/* Coalesced stores of step m's full units (unit <= J-2; unit J-1 is stored
-   exactly by its owner) from the tile; okm bit i gates instruction i. */
-template <int K>
-NA_DEV void run_store(const UniformArgs &a, const WaveIO<K> &io, const RunPlan<K> &p, uint32_t m,
-                      const uint4 *t, uint32_t lane, uint32_t okm)
-{
-    const int u = run_unit<K>(io, p.P, m);
-    if (u < 0 || u > (int)p.J - 2) return;
-    const uint32_t off = io.c16 + 64u * (uint32_t)u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint4 q = t[tile_slot(16u * i + (lane >> 2), lane & 3)];
-        const uint32_t r = wave_rec(io, i);
-        if (r < a.n_records && ((okm >> i) & 1))
-            *(uint4 *)(a.out + (size_t)r * a.out_stride + off) = q;
-    }
-}
-
-template <int K, bool UKEY>
-NA_DEV void seal_run_staged(const UniformArgs &a, uint4 *tiles, uint32_t blk)
-{
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t rec0 = ((blk * 256u + threadIdx.x) >> 6) * (64 / K);
-    const uint32_t rec_raw = rec0 + lane / K;
-    const bool live = rec_raw < a.n_records;
-    const uint32_t rc = live ? rec_raw : a.n_records - 1;
-    const int k = (int)(lane % K);
-    uint32_t key[8], n_lo, n_hi;
-    u_key_nonce<UKEY>(a, rec0, rc, key, n_lo, n_hi);
-    ChaPre pre;
-    chacha_pre(key, n_lo, n_hi, pre);
-    const uint32_t len = a.len;
-    const RunPlan<K> p = run_plan<K>(len); /* wave-uniform (uniform batch) */
-    const int gbase = (int)lane & ~(K - 1);
-    const WaveIO<K> io = wave_io<K>(rec0, lane);
-    const uint32_t v0 = (uint32_t)k * p.P;
-
-    P32 acc = p32_zero();
-    R32 r;
-    Fe r26;
-    uint32_t s[4];
-    run_dma<K>(a, io, p, 0, tiles);
-    for (uint32_t m = 0; m < p.P; ++m) {
-        const uint32_t v = v0 + m;
-        uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
-        __builtin_amdgcn_wave_barrier();
-        /* next step's bytes go into the other tile while this one computes */
-        if (m + 1 < p.P) run_dma<K>(a, io, p, m + 1, nxt);
-        uint32_t x[16];
-        chacha20_block_pre(key, pre, v, n_lo, n_hi, x);
-        if (m == 0) {
-            run_poly_key(x, gbase, r, r26, s);
-            if (k == 0 && a.ad_len) p32_ad(acc, r, u_ad(a, rc), a.ad_len);
-        }
-        __builtin_amdgcn_wave_barrier();
-        uint32_t w[16];
-        tile_get_unit(cur, lane, w);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-        if (v >= 1 && v <= p.J) {
-            uint32_t nb = 4;
-            if (v == p.J) {
-                const uint32_t bytes = len - 64 * (p.J - 1);
-                if (live) last_unit_out(u_dst(a, rc) + 64 * (p.J - 1), bytes, w);
-                mask_unit(w, bytes);
-                nb = (bytes + 15) / 16;
-            }
-            p32_unit(acc, r, w, nb);
-        }
-        tile_put_unit(cur, lane, w);
-        __builtin_amdgcn_wave_barrier();
-        run_store<K>(a, io, p, m, cur, lane, 0xfu);
-    }
-    uint32_t tag[4];
-    run_close<K>(acc, p, k, r, r26, a.ad_len, len, s, tag);
-    if (k == (int)p.kl && live) tag_out(u_dst(a, rc) + len, len, tag);
-}
-
-template <int K, bool UKEY>
-NA_DEV void open_run_staged(const UniformArgs &a, uint4 *tiles, uint32_t blk)
-{
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t rec0 = ((blk * 256u + threadIdx.x) >> 6) * (64 / K);
-    const uint32_t rec_raw = rec0 + lane / K;
-    const bool live = rec_raw < a.n_records;
-    const uint32_t rc = live ? rec_raw : a.n_records - 1;
-    const int k = (int)(lane % K);
-    uint32_t key[8], n_lo, n_hi;
-    u_key_nonce<UKEY>(a, rec0, rc, key, n_lo, n_hi);
-    ChaPre pre;
-    chacha_pre(key, n_lo, n_hi, pre);
-    const uint32_t len = a.len;
-    const RunPlan<K> p = run_plan<K>(len);
-    const int gbase = (int)lane & ~(K - 1);
-    const WaveIO<K> io = wave_io<K>(rec0, lane);
-    const uint32_t v0 = (uint32_t)k * p.P;
-    uint4 *const t0 = tiles, *const t1 = tiles + 256;
-
-    /* step-0 key stream (block 0 on lane 0: the Poly key); parked in tile 1
-       until phase 2 */
-    P32 acc = p32_zero();
-    R32 r;
-    Fe r26;
-    uint32_t s[4];
-    {
-        uint32_t x0[16];
-        chacha20_block_pre(key, pre, v0, n_lo, n_hi, x0);
-        tile_put_unit(t1, lane, x0);
-        run_poly_key(x0, gbase, r, r26, s);
-    }
-    if (k == 0 && a.ad_len) p32_ad(acc, r, u_ad(a, rc), a.ad_len);
-
-    /* phase 1: authenticate.  No ChaCha to hide behind here, so the next
-       step is register-prefetched and tile 0 alone is used. */
-    Quad Q = run_load<K>(a, io, p, 0);
-    tile_put_coalesced(t0, lane, Q);
-    for (uint32_t m = 0; m < p.P; ++m) {
-        if (a.balance) prio_by_progress(m, 3 * p.P); /* phase 1: ~1/3 of the work */
-        const uint32_t v = v0 + m;
-        Q = run_load<K>(a, io, p, m + 1 < p.P ? m + 1 : m);
-        __builtin_amdgcn_wave_barrier();
-        uint32_t w[16];
-        tile_get_unit(t0, lane, w);
-        if (v >= 1 && v <= p.J) {
-            uint32_t nb = 4;
-            if (v == p.J) {
-                const uint32_t bytes = len - 64 * (p.J - 1);
-                mask_unit(w, bytes);
-                nb = (bytes + 15) / 16;
-            }
-            p32_unit(acc, r, w, nb);
-        }
-        __builtin_amdgcn_wave_barrier();
-        tile_put_coalesced(t0, lane, Q);
-    }
-    uint32_t tag[4], got[4];
-    run_close<K>(acc, p, k, r, r26, a.ad_len, len, s, tag);
-    tag_in<true>(u_src(a, rc), len, got);
-    const bool ok = tag_equal(tag, got);
-    if (k == (int)p.kl && live && a.status) a.status[rec_raw] = ok ? 0 : 1;
-    /* verdict of the owner each coalesced instruction serves */
-    uint32_t okm = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        okm |= (__shfl((int)ok, (int)(16u * i + (lane >> 2)), 64) != 0 ? 1u : 0u) << i;
-
-    /* phase 2: decrypt, double-buffered by LDS-DMA (the step-0 key stream
-       leaves tile 1 before the first DMA into it) */
-    __builtin_amdgcn_wave_barrier();
-    run_dma<K>(a, io, p, 0, t0);
-    for (uint32_t m = 0; m < p.P; ++m) {
-        if (a.balance) prio_by_progress(p.P + 2 * m, 3 * p.P);
-        const uint32_t v = v0 + m;
-        uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
-        uint32_t x[16];
-        if (m == 0) {
-            tile_get_unit(t1, lane, x);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (m + 1 < p.P) run_dma<K>(a, io, p, m + 1, nxt);
-        if (m != 0) chacha20_block_pre(key, pre, v, n_lo, n_hi, x);
-        __builtin_amdgcn_wave_barrier();
-        uint32_t w[16];
-        tile_get_unit(cur, lane, w);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-        if (v >= 1 && v == p.J && live && ok)
-            last_unit_out(u_dst(a, rc) + 64 * (p.J - 1), len - 64 * (p.J - 1), w);
-        tile_put_unit(cur, lane, w);
-        __builtin_amdgcn_wave_barrier();
-        run_store<K>(a, io, p, m, cur, lane, okm);
-    }
-}
-
 NA_DEV void p32_ad(P32 &acc, const R32 &r, const uint8_t *ad, uint32_t ad_len)
 {
     for (uint32_t off = 0; off < ad_len; off += 16) {
@@ -1463,56 +1141,20 @@ NA_DEV RecView ragged_view(const RaggedArgs &a, uint32_t rec)
 }
 
 /* LDS-staged uniform FAST batches, K = 4 or 8 lanes per record */
-/* NA_RUN_STAGED (default 1): the uniform FAST kernels use the contiguous-run
-   decomposition with radix-2^32 Poly1305; 0 = the interleaved one (A/B). */
-#ifndef NA_RUN_STAGED
-#define NA_RUN_STAGED 0
-#endif
-
-template <int K, bool UKEY>
-NA_DEV void seal_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uint32_t blk)
-{
-#if NA_RUN_STAGED
-    (void)fin;
-    seal_run_staged<K, UKEY>(a, tiles, blk);
-#else
-    seal_il_staged<K, UKEY>(a, tiles, fin, blk);
-#endif
-}
-
-template <int K, bool UKEY>
-NA_DEV void open_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uint32_t blk)
-{
-#if NA_RUN_STAGED
-    (void)fin;
-    open_run_staged<K, UKEY>(a, tiles, blk);
-#else
-    open_il_staged<K, UKEY>(a, tiles, fin, blk);
-#endif
-}
-
 template <int K, bool UKEY>
 __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_seal_staged(UniformArgs a)
 {
     __shared__ uint4 tiles[4][512]; /* two 4 KB tiles per wave */
-#if NA_RUN_STAGED
-    seal_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], nullptr, blockIdx.x);
-#else
     __shared__ FinSlot fin[4];
-    seal_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], blockIdx.x);
-#endif
+    seal_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], blockIdx.x);
 }
 
 template <int K, bool UKEY>
 __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_open_staged(UniformArgs a)
 {
     __shared__ uint4 tiles[4][512];
-#if NA_RUN_STAGED
-    open_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], nullptr, blockIdx.x);
-#else
     __shared__ FinSlot fin[4];
-    open_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], blockIdx.x);
-#endif
+    open_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], blockIdx.x);
 }
 
 /* Duplex: one launch over two independent uniform jobs — seal job `s` and
@@ -1528,11 +1170,7 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_staged(
     UniformArgs s, UniformArgs o, uint32_t s_blocks, uint32_t o_blocks)
 {
     __shared__ uint4 tiles[4][512];
-#if NA_RUN_STAGED
-    FinSlot *const fin = nullptr;
-#else
     __shared__ FinSlot fin[4];
-#endif
     const uint32_t n = min(s_blocks, o_blocks);
     uint32_t b = blockIdx.x;
     bool open;
@@ -1543,13 +1181,8 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_staged(
         open = o_blocks > s_blocks;
         b -= n;
     }
-#if NA_RUN_STAGED
-    FinSlot *const my_fin = fin;
-#else
-    FinSlot *const my_fin = &fin[threadIdx.x >> 6];
-#endif
-    if (open) open_staged<K, UKEY>(o, tiles[threadIdx.x >> 6], my_fin, b);
-    else seal_staged<K, UKEY>(s, tiles[threadIdx.x >> 6], my_fin, b);
+    if (open) open_il_staged<K, UKEY>(o, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], b);
+    else seal_il_staged<K, UKEY>(s, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], b);
 }
 
 template <int K, bool FAST>
