@@ -119,8 +119,25 @@ def stride(n: int) -> int:
     return (n + IN_ALIGN - 1) // IN_ALIGN * IN_ALIGN
 
 
+def physical_cores(cpus):
+    """Distinct physical cores (package, core id) among the logical CPUs."""
+    seen = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            with open(base + "physical_package_id") as f:
+                pkg = f.read().strip()
+            with open(base + "core_id") as f:
+                core = f.read().strip()
+        except OSError:
+            return None
+        seen.add((pkg, core))
+    return len(seen) or None
+
+
 def host_cpu():
-    """CPU model and the CPUs this process may use (SURVEY.md 8d asks for both)."""
+    """CPU model, logical CPUs, the affinity set, its physical cores and the
+    CPU share this job is given (SURVEY.md 8d asks for the core count)."""
     model = None
     try:
         with open("/proc/cpuinfo") as fh:
@@ -131,16 +148,40 @@ def host_cpu():
     except OSError:
         pass
     try:
-        usable = len(os.sched_getaffinity(0))
+        aff = sorted(os.sched_getaffinity(0))
     except AttributeError:
-        usable = os.cpu_count() or 1
-    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+        aff = list(range(os.cpu_count() or 1))
+    share = os.environ.get("OMP_NUM_THREADS")
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": len(aff),
+            "physical_cores": physical_cores(aff),
+            "cpu_share": int(share) if share and share.isdigit() else None}
 
 
 def cpu_baseline(cfg, budget_cpu_s: float = 12.0):
-    """Reference noise-c (oracle/_ref/ref_bench), bounded sample."""
+    """Reference noise-c on this host's cores, bounded sample."""
     r = _cpu_baseline(cfg, budget_cpu_s)
     return None if r is None else {**r, **host_cpu()}
+
+
+def ref_perf_cipher(path, timeout_s=120.0):
+    """Run the reference's tests/performance program (oracle/_ref/
+    test-performance, built from its own sources) and read its ChaChaPoly and
+    AESGCM perf_cipher lines (MiB/s; test-performance.c:140-179, 420-422).
+    It goes on to time DH and signatures, which this baseline does not need:
+    once both cipher lines are out the child is stopped (by its own PID)."""
+    p = subprocess.Popen([path], stdout=subprocess.PIPE, text=True)
+    out, t0 = {}, time.time()
+    try:
+        for line in p.stdout:
+            f = line.split()
+            if len(f) >= 3 and f[0] in ("ChaChaPoly", "AESGCM"):
+                out[f[0]] = float(f[1])
+            if len(out) == 2 or time.time() - t0 > timeout_s:
+                break
+    finally:
+        p.kill()
+        p.wait()
+    return out
 
 
 def _cpu_baseline(cfg, budget_cpu_s):
@@ -152,18 +193,33 @@ def _cpu_baseline(cfg, budget_cpu_s):
     if not os.path.exists(ref):
         return None
     cname = "aesgcm" if cfg["cipher"] == AES else "chachapoly"
-    if cfg.get("ad"):  # the reference's own perf_cipher loop, unchanged: 1 thread, encrypt only
+    if cfg.get("ad"):
+        # the reference's own tests/performance program, unchanged: 1 thread,
+        # 200 MiB of 1024-B records with 32 B AD, encrypt only, CPU-time clock
+        tp = os.path.join(ROOT, "oracle", "_ref", "test-performance")
+        if os.path.exists(tp):
+            r = ref_perf_cipher(tp)
+            name = "AESGCM" if cfg["cipher"] == AES else "ChaChaPoly"
+            return {"value": round(r[name] / 1024.0, 4), "unit": "GiB/s", "cores": 1,
+                    "kind": "reference",
+                    "sample": f"noise-c tests/performance/test-performance (built from the reference's "
+                              f"sources, run unchanged): perf_cipher {name}, 200 MiB of 1024 B + 32 B AD "
+                              f"encrypts, one thread, CPU-time clock (encrypt only); its AESGCM/ChaChaPoly "
+                              f"lines: {r}"}
         out = subprocess.run([ref, "perf", cname, str(cfg["len"]), "200000", "1"],
                              capture_output=True, text=True, timeout=300, check=True)
         r = json.loads(out.stdout)
         return {"value": round(r["mib_per_s"] / 1024.0, 4), "unit": "GiB/s", "cores": 1,
-                "kind": kind, "sample": f"tests/performance perf_cipher {cname}: 200000 x "
-                f"1024 B + 32 B AD encrypts, one thread, CPU-time clock (encrypt only)"}
-    try:
-        ncpu = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))
+                "kind": kind, "sample": f"{'reference library' if kind == 'reference' else 'oracle port'} "
+                f"in a restatement of perf_cipher's loop (oracle/ref_bench.c perf; the reference's "
+                f"test-performance binary was not built): 200000 x 1024 B + 32 B AD encrypts, one "
+                f"thread, CPU-time clock (encrypt only)"}
+    hc = host_cpu()
+    usable, phys = hc["usable_cpus"], hc["physical_cores"] or hc["usable_cpus"]
+    # one thread per physical core of the affinity set, within the CPU share
+    # this job is given on the box (OMP_NUM_THREADS: 16 of the host's cores
+    # per GPU on the pool; other jobs share the host)
+    threads = max(1, min(phys, usable, hc["cpu_share"] or phys))
     # calibrate on one thread (~0.3 s), then size the sample to the budget
     probe_n = 200 if cfg["cipher"] == AES else 2000
     out = subprocess.run([ref, "roundtrip", cname, str(cfg["len"]), str(probe_n), "1"],
@@ -177,13 +233,19 @@ def _cpu_baseline(cfg, budget_cpu_s):
     one = subprocess.run([ref, "roundtrip", cname, str(cfg["len"]), str(max(probe_n, int(rec_per_s * 2))), "1"],
                          capture_output=True, text=True, timeout=120, check=True)
     r1 = json.loads(one.stdout)
-    return {"value": round(r["gib_per_s"], 4), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "single_thread": round(r1["gib_per_s"], 4),
-            "sample": (f"{'noise-c ref backend CipherState API' if kind == 'reference' else 'oracle restatement'}"
-                       f" {cname}: {threads} threads x {per_thread} records x {cfg['len']} B, each "
-                       f"encrypted then decrypted+verified (send/recv CipherState pair per thread), "
-                       f"wall clock; 1 thread: {r1['gib_per_s']:.3f} GiB/s"),
-            "ok": r["ok"]}
+    res = {"value": round(r["gib_per_s"], 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+           "single_thread": round(r1["gib_per_s"], 4),
+           "sample": (f"{'noise-c ref backend CipherState API' if kind == 'reference' else 'oracle restatement'}"
+                      f" {cname}: {threads} threads (one per physical core, within this job's CPU share) x "
+                      f"{per_thread} records x {cfg['len']} B, each encrypted then decrypted+verified "
+                      f"(send/recv CipherState pair per thread), wall clock; 1 thread: "
+                      f"{r1['gib_per_s']:.3f} GiB/s"),
+           "ok": r["ok"]}
+    if phys > threads:
+        # not run (the box gives this job `threads` cores): per-thread rate x
+        # the affinity set's physical cores, an upper bound for linear scaling
+        res["all_physical_cores_linear_estimate"] = round(r["gib_per_s"] / threads * phys, 3)
+    return res
 
 
 def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length, duplex=False):
@@ -245,6 +307,8 @@ def main():
     ap.add_argument("--no-xfer", action="store_true",
                     help="skip the N>1 scatter/seal/gather leg (RCCL, SURVEY.md 8e)")
     ap.add_argument("--xfer-reps", type=int, default=5)
+    ap.add_argument("--n1-value", type=float, default=None,
+                    help="value of the same config at N = 1: adds per_gpu_efficiency for N > 1")
     ap.add_argument("--mode", default="duplex", choices=("duplex", "separate"),
                     help="duplex: each step seals one set and opens another in ONE launch "
                          "(noise_aead_dev_duplex_uniform); separate: a seal launch then an open launch")
@@ -504,6 +568,23 @@ def main():
             result["cpu_baseline"] = cpu_baseline(cfg)
         except Exception as e:  # reported, never fatal to the GPU number
             result["cpu_baseline"] = {"error": str(e)}
+    finish(args, result, rank, world, dist)
+
+
+def finish(args, result, rank, world, dist):
+    """Per-GPU efficiency when an N = 1 value is given, the
+    rehearsal label, then rank 0 prints the one JSON line."""
+    if args.n1_value and world > 1:
+        # (aggregate GiB/s at N) / (N x GiB/s at N = 1), for weak and strong
+        # scaling alike (strong: total work fixed, so this is speedup / N)
+        result["per_gpu_efficiency"] = round(result["value"] / (world * args.n1_value), 4)
+        result["n1_value"] = args.n1_value
+    if REHEARSE and world > 1:
+        # every rank on one GPU, collectives on gloo: exercises the N > 1 code
+        # path only; per-kernel rates of ranks sharing a GPU mean nothing
+        result.pop("roofline", None)
+        result["rehearsal"] = (f"{world} ranks on ONE GPU, gloo process group (collectives via host "
+                               "memory): a code-path rehearsal, not a multi-GPU measurement")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
@@ -621,10 +702,12 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                            bytes=int(lay["lens"][idx].sum()), states=len(states)))
     torch.cuda.synchronize(dev)
 
-    def launch(g, open_, stream=sp):
+    def launch(g, open_, stream=sp, inp=None, out=None):
+        inp = inp if inp is not None else (ct if open_ else pt)
+        out = out if out is not None else (back if open_ else ct)
         return A.dev_ragged(open_, g["cipher"], ctx_base=g["ctx"].data_ptr(),
-                            recs=g["recs"].data_ptr(), inp=(ct if open_ else pt).data_ptr(),
-                            out=(back if open_ else ct).data_ptr(), n_records=g["n"],
+                            recs=g["recs"].data_ptr(), inp=inp.data_ptr(),
+                            out=out.data_ptr(), n_records=g["n"],
                             status=g["st"].data_ptr() if open_ else 0, lanes=args.lanes,
                             flags=A.FLAG_FAST, stream=stream)
 
@@ -715,10 +798,87 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                        for m, gg, o in per},
         "all_tags_verified": ok,
     }
+    if world > 1 and not args.no_xfer:
+        try:  # reported beside the value; a failure here never voids the bench line
+            result["scatter_gather"] = xfer_leg_mixed(args, torch, dist, dev, A, rank, world, R, S,
+                                                      lay, pt, groups, launch)
+        except Exception as e:
+            result["scatter_gather"] = {"error": repr(e)}
+    finish(args, result, rank, world, dist)
+
+
+def xfer_leg_mixed(args, torch, dist, dev, A, rank, world, R, S, lay, pt, groups, launch):
+    """The C5 form of xfer_leg: rank 0 holds every rank's
+    ragged plaintext shard, RCCL scatters them (shards differ in size, so each
+    travels in a slot of the largest shard's size), every rank seals its own
+    records of both ciphers, RCCL gathers the sealed shards back.  The record
+    descriptors are not sent: each rank derives its own from the shared layout
+    rule (mixed_layout).  Timed per phase, max over ranks; verified."""
+    from distribute import scatter_records, gather_records
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    totals = [mixed_layout(R, S, g)["total"] for g in range(world)]
+    slot = (max(totals) + 63) // 64 * 64
+    full_in = full_out = None
     if rank == 0:
-        print(json.dumps(result), flush=True)
-    if dist:
-        dist.destroy_process_group()
+        full_in = torch.zeros(world * slot, dtype=torch.uint8, device=dev)
+        full_out = torch.zeros(world * slot, dtype=torch.uint8, device=dev)
+        for g in range(world):  # slot g = rank g's plaintext (its SplitMix64 words)
+            assert A.dev_fill_splitmix(full_in[g * slot:].data_ptr(), totals[g], SEED_PT, g << 40, sp) == 0
+    local_in = torch.zeros(slot, dtype=torch.uint8, device=dev)
+    local_out = torch.zeros(slot, dtype=torch.uint8, device=dev)
+    phases = []
+    for rep in range(args.xfer_reps + 1):
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        if REHEARSE:
+            tmp = torch.empty(slot, dtype=torch.uint8)
+            scatter_records(tmp, full_in.cpu() if rank == 0 else None, src=0)
+            local_in.copy_(tmp)
+        else:
+            scatter_records(local_in, full_in, src=0)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for g in groups:
+            if launch(g, False, inp=local_in, out=local_out):
+                raise RuntimeError("seal launch failed")
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        if REHEARSE:
+            tmp = torch.empty(world * slot, dtype=torch.uint8) if rank == 0 else None
+            gather_records(local_out.cpu(), tmp, dst=0)
+            if rank == 0:
+                full_out.copy_(tmp)
+        else:
+            gather_records(local_out, full_out, dst=0)
+        torch.cuda.synchronize(dev)
+        t3 = time.perf_counter()
+        if rep:
+            phases.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0))
+    ph = cpu_if_rehearsal(torch.tensor(phases, dtype=torch.float64, device=dev).mean(0))
+    dist.all_reduce(ph, op=dist.ReduceOp.MAX)
+    total = lay["total"]
+    ok = cpu_if_rehearsal(torch.tensor([1 if torch.equal(local_in[:total], pt[:total]) else 0],
+                                       device=dev))
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    mine = cpu_if_rehearsal(local_out.view(torch.int64).sum().reshape(1))
+    sums = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(sums, mine)
+    good = bool(ok.item())
+    if rank == 0:
+        for g in range(world):
+            got = full_out[g * slot:(g + 1) * slot].view(torch.int64).sum()
+            good &= bool(got.item() == sums[g].item())
+    sc, se, ga, tot = (float(x) * 1e3 for x in ph.tolist())
+    payload = sum(int(mixed_layout(R, S, g)["lens"].sum()) for g in range(world))
+    return {"collective": ("torch.distributed scatter/gather on gloo via host memory (one-GPU rehearsal)"
+                           if REHEARSE else
+                           "torch.distributed scatter/gather on nccl (RCCL grouped send/recv over xGMI)"),
+            "src_dst_rank": 0, "slot_bytes": slot, "shard_bytes": totals,
+            "scatter_ms": round(sc, 4), "seal_ms": round(se, 4), "gather_ms": round(ga, 4),
+            "total_ms": round(tot, 4),
+            "seal_gibs_incl_xfer": round(payload / (tot * 1e-3) / GIB, 2),
+            "verified": good, "reps": args.xfer_reps}
 
 
 if __name__ == "__main__":

@@ -378,22 +378,59 @@ NA_DEV void load16(const uint8_t *p, uint32_t n, uint32_t w[4])
     }
 }
 
+/* word q (0..3, runtime) of w without dynamic indexing */
+NA_DEV uint32_t pick_word(const uint32_t w[4], uint32_t q)
+{
+    return q == 0 ? w[0] : (q == 1 ? w[1] : (q == 2 ? w[2] : w[3]));
+}
+
+/* Store the first n (0..16) bytes of w at p, in the widest pieces p's
+   alignment allows: a record's partial last block (len % 16 bytes) and an
+   unaligned tag.  Single-byte stores only for an odd address or an odd
+   remainder — a run of them costs a partial-line write each (round 1 wrote
+   a 1400-B record's last 8 bytes as 8 byte stores: C3 seal wrote 1.47x its
+   algorithmic bytes). */
 NA_DEV void store16(uint8_t *p, uint32_t n, const uint32_t w[4])
 {
     const uintptr_t a = (uintptr_t)p;
     if (n >= 16 && (a & 15) == 0) {
         *(uint4 *)p = make_uint4(w[0], w[1], w[2], w[3]);
-    } else if (n >= 16 && (a & 7) == 0) {
-        *(uint2 *)p = make_uint2(w[0], w[1]);
-        *(uint2 *)(p + 8) = make_uint2(w[2], w[3]);
-    } else if (n >= 16 && (a & 3) == 0) {
-        uint32_t *q = (uint32_t *)p;
-        q[0] = w[0]; q[1] = w[1]; q[2] = w[2]; q[3] = w[3];
+        return;
+    }
+    if (n > 16) n = 16;
+    const uint32_t q = n >> 2; /* whole words */
+    if ((a & 3) == 0) {
+        if ((a & 7) == 0) {
+            if (q >= 2) *(uint2 *)p = make_uint2(w[0], w[1]);
+            if (q == 4) *(uint2 *)(p + 8) = make_uint2(w[2], w[3]);
+            else if (q == 3) *(uint32_t *)(p + 8) = w[2];
+            else if (q == 1) *(uint32_t *)p = w[0];
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i)
+                if (i < q) ((uint32_t *)p)[i] = w[i];
+        }
+    } else if ((a & 1) == 0) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+            if (i < q) {
+                ((uint16_t *)(p + 4 * i))[0] = (uint16_t)w[i];
+                ((uint16_t *)(p + 4 * i))[1] = (uint16_t)(w[i] >> 16);
+            }
     } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            int rem = (int)n - 4 * i;
-            st_bytes(p + 4 * i, w[i], rem <= 0 ? 0u : (rem >= 4 ? 4u : (uint32_t)rem));
+        for (uint32_t i = 0; i < 4; ++i)
+            if (i < q) st_bytes(p + 4 * i, w[i], 4);
+    }
+    const uint32_t r = n & 3; /* 0..3 trailing bytes of word q */
+    if (r) {
+        const uint32_t v = pick_word(w, q);
+        uint8_t *t = p + 4 * q;
+        if (((a & 1) == 0) && r >= 2) {
+            *(uint16_t *)t = (uint16_t)v;
+            if (r == 3) t[2] = (uint8_t)(v >> 16);
+        } else {
+            st_bytes(t, v, r);
         }
     }
 }

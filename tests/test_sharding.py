@@ -122,3 +122,96 @@ def test_two_rank_scatter_seal_gather():
     pt = o.fill(0x7074, world * R * L, 0)
     expect = b"".join(o.encrypt(0x4301, key, i, pt[i * L:(i + 1) * L]) for i in range(world * R))
     assert got == expect
+
+
+def test_c4_strong_shards_equal_one_gpu_layout():
+    """C4 is strong scaling (bench.py: records and states divided by N): the
+    ranks' (state key id, nonce) sets of N = 2 and 4 are exactly the N = 1
+    layout's, each state's whole nonce run on one rank."""
+    sys.path.insert(0, ROOT)
+    import bench
+    N, S = 1024, 64  # 1 Mi / 4096 scaled down, 16 records per state
+    one = bench.shard(N, S, 0, 1)
+    ref = {(one["key_ids"][i // one["rps"]], one["nonce_base"][i // one["rps"]] + i % one["rps"])
+           for i in range(N)}
+    for world in (2, 4):
+        got, owner = set(), {}
+        for r in range(world):
+            sh = bench.shard(N // world, S // world, r, world)
+            assert sh["rps"] == one["rps"]
+            for i in range(sh["count"]):
+                kid = sh["key_ids"][i // sh["rps"]]
+                assert owner.setdefault(kid, r) == r, "a state's records split over ranks"
+                got.add((kid, sh["nonce_base"][i // sh["rps"]] + i % sh["rps"]))
+        assert got == ref
+
+
+def _c5_records(rank, world, R, S, sample):
+    """(global record, len, global state, nonce, cipher, tag hash) of a sample
+    of rank's C5 records, sealed by the oracle as the GPU rank would."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bench
+    from oracle import Oracle
+    o = Oracle()
+    lay = bench.mixed_layout(R, S, rank)
+    out = []
+    for j in sample:
+        L, st, n = int(lay["lens"][j]), int(lay["st_global"][j]), int(lay["nonce"][j])
+        cipher = 0x4301 if st % 2 == 0 else 0x4302
+        key = o.fill(bench.SEED_KEY, 32, 4 * st)
+        # plaintext at the rank's own byte offset of its own SplitMix64 stream
+        pt = o.fill(bench.SEED_PT, lay["off"][j] + L + 8, rank << 40)[lay["off"][j]:lay["off"][j] + L]
+        tag = o.encrypt(cipher, key, n, pt)[-16:]
+        out.append((rank * R + j, L, st, n, cipher,
+                    int.from_bytes(hashlib.sha256(tag).digest()[:7], "little")))
+    return out
+
+
+def _c5_worker(rank, world, port, R, S, sample, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = torch.tensor(_c5_records(rank, world, R, S, sample), dtype=torch.int64)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    if rank == 0:
+        q.put(torch.cat(parts).tolist())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_c5_ragged_shards():
+    """C5 (mixed ChaChaPoly/AESGCM, 64 B-16 KiB records): rank r's shard is
+    records [rR, (r+1)R) and states [rS, (r+1)S) of the global job; record
+    lengths, state, cipher and nonce of every record equal those of the
+    one-process layout of the whole job (mixed_layout over 2R records, 2S
+    states), and the sampled records' oracle tags agree, gathered over gloo."""
+    sys.path.insert(0, ROOT)
+    import bench
+    world, R, S = 2, 64, 8
+    whole = bench.mixed_layout(world * R, world * S, 0)
+    for r in range(world):
+        lay = bench.mixed_layout(R, S, r)
+        sl = slice(r * R, (r + 1) * R)
+        assert (lay["lens"] == whole["lens"][sl]).all()
+        assert (lay["st_global"] == whole["st_global"][sl]).all()
+        assert (lay["nonce"] == whole["nonce"][sl]).all()
+    sample = [0, 1, R // S - 1, R // S, R - 1]  # state edges
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29900 + os.getpid() % 1000
+    procs = [ctx.Process(target=_c5_worker, args=(r, world, port, R, S, sample, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = []
+    for r in range(world):
+        expect += [list(t) for t in _c5_records(r, world, R, S, sample)]
+    assert got == expect
+    # every (state, nonce) pair is used once over the whole job
+    pairs = {(int(whole["st_global"][i]), int(whole["nonce"][i])) for i in range(world * R)}
+    assert len(pairs) == world * R
