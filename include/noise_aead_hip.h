@@ -243,7 +243,11 @@ typedef struct NoiseAeadRagged {
     uint32_t reserved_;
 } NoiseAeadRagged;
 
-/* The caller guarantees, for every record: in + in_off and out + out_off are
+/* A record longer than NOISE_MAX_PAYLOAD_LEN - 16 (65519) bytes is not
+ * processed: nothing is written and, when status is given, status[i] = 2 —
+ * for seal too (status is optional there: 0 sealed, 2 refused).
+ *
+ * The caller guarantees, for every record: in + in_off and out + out_off are
  * 16-byte aligned, and the input may be read up to roundup64(max(len, 1))
  * bytes (and holds CT || tag for open).  Enables the straight-line dwordx4 path.  The
  * uniform API derives this itself from the pointers and strides. */
@@ -284,6 +288,23 @@ int noise_aead_dev_encrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
                                     const NoiseAeadRagged *job, void *stream);
 int noise_aead_dev_decrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
                                     const NoiseAeadRagged *job, void *stream);
+
+/* ------------------------------------------------ error reports
+ * include/noise/protocol/errors.h; src/protocol/errors.c:92-127. */
+void noise_perror(const char *s, int err);
+int noise_strerror(int err, char *buf, size_t size);
+
+/* ------------------------------------------------ test / debug hooks
+ * Not part of the reference surface; used by the test suite.
+ * noise_aead_debug_batch_stats: GPU rounds and records dispatched by this
+ *   thread's last noise_cipherstate_decrypt_batch call (a run of forged
+ *   records must cost rounds, not re-dispatches of the whole batch).
+ * noise_aead_debug_last_freed_ctx: with NOISE_AEAD_DEBUG_KEEP_FREED=1 in the
+ *   environment, freeing a CipherState scrubs its device key context but keeps
+ *   the allocation; this returns it (and its size) so a test can read back
+ *   zeros.  Leaks by design; never set it in production. */
+void noise_aead_debug_batch_stats(uint64_t *rounds, uint64_t *dispatched);
+void *noise_aead_debug_last_freed_ctx(size_t *bytes);
 
 /* Default lanes per record the library picks for a batch of n records. */
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records);

@@ -23,24 +23,33 @@ using namespace na;
 namespace {
 
 constexpr int kMaxDevices = 64;
-std::once_flag g_tab_once[kMaxDevices];
-hipError_t g_tab_err[kMaxDevices];
+std::mutex g_tab_mu[kMaxDevices];
+bool g_tab_ready[kMaxDevices];
 
 int hip_rc(hipError_t e) { return e == hipSuccess ? NOISE_ERROR_NONE : NOISE_ERROR_SYSTEM; }
 
-/* S-box / T-table are generated on each device once (aesgcm.hip). */
-hipError_t ensure_aes_tables(hipStream_t stream)
+/* S-box / T-table are generated on each device once (aesgcm.hip), on a
+   private stream — never the caller's, which may be capturing a graph —
+   and waited for.  Only success is remembered: after a failure the next AES
+   call on that device tries again. */
+hipError_t ensure_aes_tables(hipStream_t)
 {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
-    std::call_once(g_tab_once[dev], [&] {
-        hipLaunchKernelGGL(aes_tables_init, dim3(1), dim3(256), 0, stream);
-        g_tab_err[dev] = hipGetLastError();
-        if (g_tab_err[dev] == hipSuccess) g_tab_err[dev] = hipStreamSynchronize(stream);
-    });
-    return g_tab_err[dev];
+    if (__atomic_load_n(&g_tab_ready[dev], __ATOMIC_ACQUIRE)) return hipSuccess;
+    std::lock_guard<std::mutex> lk(g_tab_mu[dev]);
+    if (g_tab_ready[dev]) return hipSuccess;
+    hipStream_t s = nullptr;
+    e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(aes_tables_init, dim3(1), dim3(256), 0, s);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    if (e == hipSuccess) __atomic_store_n(&g_tab_ready[dev], true, __ATOMIC_RELEASE);
+    return e;
 }
 
 /* Lanes per record for ChaChaPoly: 4 (the fastest split at 64 Ki and 1 Mi
@@ -488,13 +497,15 @@ int noise_aead_dev_decrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
     hipStream_t s = (hipStream_t)stream;
     const size_t bytes = (size_t)job->n_records * hl;
     uint8_t *h_new = nullptr;
+    /* stream-ordered pool allocation: no device synchronisation, and after
+       the first call the pool hands the same memory back */
     if (hipMallocAsync((void **)&h_new, bytes, s) != hipSuccess) return NOISE_ERROR_NO_MEMORY;
     /* hash the ciphertext before the (in-place) decryption overwrites it */
     int rc = launch_mix_hash(hash_id, hl, d_h, h_new, job, false, s);
     if (!rc) rc = run_ragged(cipher_id, job, stream, true);
     if (!rc) {
-        const uint32_t total = job->n_records * hl;
-        hipLaunchKernelGGL(commit_hash, dim3((total + 255) / 256), dim3(256), 0, s, d_h,
+        const uint64_t total = (uint64_t)job->n_records * hl;
+        hipLaunchKernelGGL(commit_hash, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, d_h,
                            (const uint8_t *)h_new, (const uint8_t *)job->status, hl,
                            job->n_records);
         rc = hip_rc(hipGetLastError());

@@ -44,9 +44,26 @@ struct RaggedArgs {
     const uint8_t *in;
     uint8_t *out;
     const uint8_t *ad;
-    uint8_t *status;
+    uint8_t *status;   /* open: per record 0 ok / 1 MAC failure / 2 bad length;
+                          seal (optional): 0 / 2 */
     uint32_t n_records;
 };
+
+/* A ragged descriptor's record longer than NOISE_MAX_PAYLOAD_LEN - 16 bytes
+   (constants.h:151; cipherstate.c:307,313,382 refuse it) is not processed:
+   nothing is written and status (when given) is 2.  The AES-GCM kernels
+   also rely on it: their CTR counter stays below 2^16. */
+constexpr uint32_t MAX_RECORD_LEN = 65535 - 16;
+constexpr uint8_t STATUS_BAD_LENGTH = 2;
+
+/* Called by every lane of record `rec` (the group leaves together). */
+__device__ __forceinline__ bool reject_len(const RaggedArgs &a, uint32_t rec, uint32_t len,
+                                           bool writer)
+{
+    if (len <= MAX_RECORD_LEN) return false;
+    if (writer && a.status) a.status[rec] = STATUS_BAD_LENGTH;
+    return true;
+}
 
 /* Length-balanced record order for a workgroup of a ragged batch.  A wave is
    as slow as its longest record, so the NREC records of the workgroup's
@@ -64,7 +81,7 @@ __device__ __forceinline__ uint32_t window_rec(const RecDesc *recs, uint32_t n, 
     const uint32_t t = threadIdx.x, nt = blockDim.x;
     for (uint32_t i = t; i < (uint32_t)NREC; i += nt) {
         const uint32_t rec = base + i;
-        keys[i] = rec < n ? (recs[rec].len << 8) | i : 0xFFFFFFFFu; /* len <= 65519 */
+        keys[i] = rec < n ? (min(recs[rec].len, 65535u) << 8) | i : 0xFFFFFFFFu; /* 24-bit len key */
     }
     __syncthreads();
     for (uint32_t k = 2; k <= (uint32_t)NREC; k <<= 1)

@@ -359,6 +359,7 @@ __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
     if (rec >= a.n_records) return;
     const int l = (int)(threadIdx.x % GCM_LANES);
     const RecDesc d = a.recs[rec];
+    if (reject_len(a, rec, d.len, l == GCM_LANES - 1)) return;
     GcmView rv;
     rv.src = a.in + d.in_off;
     rv.dst = a.out + d.out_off;
@@ -368,7 +369,7 @@ __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
     rv.len = d.len;
     rv.ad_len = d.ad_len;
     const bool ok = gcm_record<OPEN>(rv, l, te, sb);
-    if (OPEN && l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
 /* ---------------------------- staged (uniform FAST, one state per workgroup)
@@ -782,6 +783,7 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t tpl = (1u << 16) | ((128u + 4u * (lane & 31)) << 8) | (4u * (lane & 31));
     const RecDesc d = a.recs[rec];
+    if (reject_len(a, rec, d.len, l == K - 1)) return;
     GcmView rv;
     rv.src = a.in + d.in_off;
     rv.dst = a.out + d.out_off;
@@ -796,7 +798,7 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
         ok = gcm_record_staged<OPEN, FAST>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
     else /* a third state in the window: its own context, from global memory */
         ok = gcm_record_global<OPEN, FAST>(rv, l, TE, tpl);
-    if (OPEN && l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
 /* ------------------------------------------ wide (small batches, latency)
@@ -817,6 +819,7 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
     __shared__ uint32_t verdict;
     const uint32_t rec = blockIdx.x, t = threadIdx.x;
     const RecDesc d = a.recs[rec];
+    if (reject_len(a, rec, d.len, t == 0)) return; /* uniform over the workgroup */
     const AesCtx *ctx = (const AesCtx *)(a.keys + d.ctx_off);
     const uint8_t *src = a.in + d.in_off;
     uint8_t *dst = a.out + d.out_off;
@@ -874,6 +877,7 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
         const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
         if (!OPEN) {
             if (l == K - 1) store16(dst + len, 16, tag);
+            if (l == K - 1 && a.status) a.status[rec] = 0;
         } else if (l == 0) {
             uint32_t got[4];
             load16(src + len, 16, got);

@@ -1214,7 +1214,10 @@ __global__ __launch_bounds__(256) void chachapoly_seal_ragged(RaggedArgs a)
     const uint32_t rec = window_rec<256 / K>(a.recs, a.n_records, blockIdx.x * (256u / K),
                                              threadIdx.x / K, order);
     if (rec >= a.n_records) return;
-    seal_any<K, FAST>(ragged_view(a, rec), (int)(threadIdx.x % K));
+    const RecView rv = ragged_view(a, rec);
+    if (reject_len(a, rec, rv.len, threadIdx.x % K == K - 1)) return;
+    seal_any<K, FAST>(rv, (int)(threadIdx.x % K));
+    if (threadIdx.x % K == K - 1 && a.status) a.status[rec] = 0;
 }
 
 template <int K, bool FAST>
@@ -1225,13 +1228,15 @@ __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
                                              threadIdx.x / K, order);
     if (rec >= a.n_records) return;
     const int k = (int)(threadIdx.x % K);
+    const RecView rv = ragged_view(a, rec);
+    if (reject_len(a, rec, rv.len, k == K - 1)) return;
     bool ok;
     if constexpr (FAST && K >= 4) {
         __shared__ uint4 r0[4][256], r1[4][256], r2[4][256]; /* 3 x 4 KB per wave */
         const uint32_t w = threadIdx.x >> 6;
-        ok = open_il<K, true, true>(ragged_view(a, rec), k, AuthRing{r0[w], r1[w], r2[w]});
+        ok = open_il<K, true, true>(rv, k, AuthRing{r0[w], r1[w], r2[w]});
     } else {
-        ok = open_any<K, FAST>(ragged_view(a, rec), k);
+        ok = open_any<K, FAST>(rv, k);
     }
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }

@@ -120,16 +120,61 @@ Staging *na_stage_get(size_t bytes)
 /* --------------------------------------------------- device key contexts */
 
 
+/* Zero n bytes of device memory on `device` and wait for it, so that key
+   material is gone before the allocation can be handed out again
+   (util.c:152-158 zeroes every freed object).  Restores the current device. */
+static void scrub_device(void *p, size_t n, int device)
+{
+    if (!p || !n) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    if (hipMemsetAsync(p, 0, n, NULL) == hipSuccess) (void)hipStreamSynchronize(NULL);
+    if (cur != device) (void)hipSetDevice(cur);
+}
+
+/* Test hook (NOISE_AEAD_DEBUG_KEEP_FREED=1): destroy scrubs a state's device
+   context but keeps the allocation, so a test can read back that it was
+   zeroed.  Leaks by design; never set in production. */
+static void *g_dbg_freed_ctx;
+static size_t g_dbg_freed_bytes;
+
+void *noise_aead_debug_last_freed_ctx(size_t *bytes)
+{
+    if (bytes) *bytes = g_dbg_freed_bytes;
+    return g_dbg_freed_ctx;
+}
+
+static void release_ctx(HipCipherState *st)
+{
+    if (!st->d_ctx) return;
+    const size_t bytes = noise_aead_dev_ctx_bytes(st->parent.cipher_id);
+    scrub_device(st->d_ctx, bytes, st->device); /* the context holds key material */
+    const char *keep = getenv("NOISE_AEAD_DEBUG_KEEP_FREED");
+    if (keep && *keep == '1') {
+        g_dbg_freed_ctx = st->d_ctx;
+        g_dbg_freed_bytes = bytes;
+    } else {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != st->device) (void)hipSetDevice(st->device);
+        (void)hipFree(st->d_ctx);
+        if (cur != st->device) (void)hipSetDevice(cur);
+    }
+    st->d_ctx = NULL;
+    st->ctx_ready = 0;
+}
+
 /* Build the device key context of `st` from its key (lazy: init_key has no
-   error return in the plugin ABI, internal.h:95). */
+   error return in the plugin ABI, internal.h:95).  A context belongs to the
+   device it was built on: used from another device it is scrubbed and
+   rebuilt there, never passed to a kernel on the wrong device. */
 int na_ensure_ctx(HipCipherState *st, Staging *sg)
 {
-    if (st->ctx_ready) return NOISE_ERROR_NONE;
-    int dev = sg->device;
-    if (st->d_ctx && st->device != dev) {
-        (void)hipFree(st->d_ctx);
-        st->d_ctx = NULL;
-    }
+    const int dev = sg->device;
+    if (st->ctx_ready && st->d_ctx && st->device == dev) return NOISE_ERROR_NONE;
+    if (st->d_ctx && st->device != dev) release_ctx(st);
+    st->ctx_ready = 0;
     if (!st->d_ctx) {
         size_t bytes = noise_aead_dev_ctx_bytes(st->parent.cipher_id);
         if (hipMalloc(&st->d_ctx, bytes) != hipSuccess) {
@@ -138,16 +183,19 @@ int na_ensure_ctx(HipCipherState *st, Staging *sg)
         }
         st->device = dev;
     }
-    /* raw key through the tail of the staging area */
+    /* raw key through the tail of the staging area; both copies are zeroed
+       again on every path out */
     uint8_t *h = sg->h + sg->cap - 32;
     uint8_t *d = sg->d + sg->cap - 32;
     memcpy(h, st->key, 32);
+    int rc = NOISE_ERROR_NONE;
     if (hipMemcpyAsync(d, h, 32, hipMemcpyHostToDevice, sg->stream) != hipSuccess)
-        return NOISE_ERROR_SYSTEM;
-    int rc = noise_aead_dev_prepare(st->parent.cipher_id, d, 1, st->d_ctx, sg->stream);
-    if (rc) return rc;
-    if (hipStreamSynchronize(sg->stream) != hipSuccess) return NOISE_ERROR_SYSTEM;
+        rc = NOISE_ERROR_SYSTEM;
+    if (!rc) rc = noise_aead_dev_prepare(st->parent.cipher_id, d, 1, st->d_ctx, sg->stream);
+    (void)hipMemsetAsync(d, 0, 32, sg->stream);
+    if (hipStreamSynchronize(sg->stream) != hipSuccess && !rc) rc = NOISE_ERROR_SYSTEM;
     na_clean(h, 32);
+    if (rc) return rc;
     st->ctx_ready = 1;
     return NOISE_ERROR_NONE;
 }
@@ -335,6 +383,12 @@ static int launch_chunk(Staging *sg, const Chunk *c, int ci, int open, int zc)
                                sg->stream) != hipSuccess) ||
         hipEventRecord(sg->ev_out[ci], sg->stream) != hipSuccess)
         return NOISE_ERROR_SYSTEM;
+    /* open leaves plaintext in the device staging slots: zero them once the
+       D2H has read them (stream order), so no plaintext outlives the call in
+       device memory (a seal's slots end up holding only CT || tag) */
+    if (open && !zc &&
+        hipMemsetAsync(sg->d + c->payload_off, 0, c->end - c->payload_off, sg->stream) != hipSuccess)
+        return NOISE_ERROR_SYSTEM;
     return NOISE_ERROR_NONE;
 }
 
@@ -510,15 +564,7 @@ static int hip_decrypt(NoiseCipherState *state, const uint8_t *ad, size_t ad_len
 
 static void hip_destroy(NoiseCipherState *state)
 {
-    HipCipherState *st = (HipCipherState *)state;
-    if (st->d_ctx) {
-        int cur = 0;
-        (void)hipGetDevice(&cur);
-        if (cur != st->device) (void)hipSetDevice(st->device);
-        (void)hipFree(st->d_ctx); /* context holds key material: freed with the state */
-        if (cur != st->device) (void)hipSetDevice(cur);
-        st->d_ctx = NULL;
-    }
+    release_ctx((HipCipherState *)state); /* scrubbed, then freed with the state */
 }
 
 static NoiseCipherState *hip_new(int cipher_id, NoiseCipherState *(*create)(void))
@@ -626,6 +672,7 @@ static int check_encrypt(const NoiseCipherState *state, const uint8_t *ad, size_
         *passthrough = 1;
         return NOISE_ERROR_NONE;
     }
+    if (ad_len > UINT32_MAX) return NOISE_ERROR_INVALID_LENGTH; /* device descriptors hold 32 bits */
     if (buffer->size > (size_t)(NOISE_MAX_PAYLOAD_LEN - state->mac_len))
         return NOISE_ERROR_INVALID_LENGTH;
     if ((buffer->max_size - buffer->size) < state->mac_len) return NOISE_ERROR_INVALID_LENGTH;
@@ -645,6 +692,7 @@ static int check_decrypt(const NoiseCipherState *state, const uint8_t *ad, size_
         *passthrough = 1;
         return NOISE_ERROR_NONE;
     }
+    if (ad_len > UINT32_MAX) return NOISE_ERROR_INVALID_LENGTH; /* device descriptors hold 32 bits */
     if (buffer->size < state->mac_len) return NOISE_ERROR_INVALID_LENGTH;
     return NOISE_ERROR_NONE;
 }
@@ -773,22 +821,41 @@ static void open_batch_decide(Job *jobs, size_t lo, size_t hi, void *u)
     }
 }
 
+/* Test hook: rounds and dispatched records of this thread's last
+   noise_cipherstate_decrypt_batch call. */
+static __thread uint64_t t_batch_rounds, t_batch_dispatched;
+
+void noise_aead_debug_batch_stats(uint64_t *rounds, uint64_t *dispatched)
+{
+    if (rounds) *rounds = t_batch_rounds;
+    if (dispatched) *dispatched = t_batch_dispatched;
+}
+
 int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8_t *const *ads,
                                     const size_t *ad_lens, NoiseBuffer *buffers, size_t count,
                                     int *results)
 {
     if ((!states || !buffers || !results) && count) return NOISE_ERROR_INVALID_PARAM;
     static uint64_t epoch_counter = 0;
-    Job *jobs = (Job *)malloc((count ? count : 1) * sizeof(Job));
-    size_t *pend = (size_t *)malloc((count ? count : 1) * sizeof(size_t));
-    if (!jobs || !pend) {
+    t_batch_rounds = t_batch_dispatched = 0;
+    const size_t cap = count ? count : 1;
+    Job *jobs = (Job *)malloc(cap * sizeof(Job));
+    size_t *pend = (size_t *)malloc(cap * sizeof(size_t));
+    size_t *job_of = (size_t *)malloc(cap * sizeof(size_t));
+    if (!jobs || !pend || !job_of) {
         free(jobs);
         free(pend);
+        free(job_of);
         return NOISE_ERROR_NO_MEMORY;
     }
-    /* Round 1 validates everything; records whose outcome depends on an
-       earlier MAC failure of the same state are re-run in later rounds with
-       the nonce the sequential calls would have used. */
+    /* Round 1 validates everything and dispatches every record with the
+       nonce it gets if all earlier records of its state verify.  A MAC
+       failure leaves n where it was, so that state's later records are
+       re-run in later rounds with the nonce the sequential calls would have
+       used.  After a failure a state dispatches a window of records per round
+       that restarts at 1 and doubles while they verify: a run of forged
+       records costs one small round each instead of re-running everything
+       after it every time, so the GPU work stays linear in the batch. */
     size_t np = 0;
     for (size_t i = 0; i < count; ++i) {
         NoiseCipherState *st = states[i];
@@ -801,12 +868,14 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
         int pass;
         results[i] = check_decrypt(st, ad, ad_len, &buffers[i], &pass);
         if (results[i] || pass) continue;
+        ((HipCipherState *)st)->b_window = 0;
         pend[np++] = i;
     }
     OpenBatch ob = {buffers, results};
     int rc = NOISE_ERROR_NONE;
     while (np && !rc) {
         const uint64_t epoch = __atomic_add_fetch(&epoch_counter, 1, __ATOMIC_RELAXED);
+        size_t nj = 0;
         for (size_t p = 0; p < np; ++p) {
             size_t i = pend[p];
             HipCipherState *st = (HipCipherState *)states[i];
@@ -814,8 +883,15 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
                 st->b_epoch = epoch;
                 st->b_next = st->parent.n;
                 st->b_failed = 0;
+                st->b_sent = 0;
             }
-            Job *j = &jobs[p];
+            if (st->b_window && st->b_sent >= st->b_window) { /* beyond this round's window */
+                job_of[p] = SIZE_MAX;
+                continue;
+            }
+            ++st->b_sent;
+            job_of[p] = nj;
+            Job *j = &jobs[nj++];
             j->st = st;
             j->ad = ads ? ads[i] : NULL;
             j->ad_len = ad_lens ? ad_lens[i] : 0;
@@ -828,17 +904,35 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
             j->skip = st->b_next == NONCE_LIMIT;
             if (!j->skip) ++st->b_next;
         }
-        rc = run_jobs(jobs, np, 1, open_batch_decide, &ob);
+        ++t_batch_rounds;
+        t_batch_dispatched += nj;
+        rc = run_jobs(jobs, nj, 1, open_batch_decide, &ob);
+        for (size_t k = 0; k < nj; ++k) { /* next round's window of each state */
+            HipCipherState *st = jobs[k].st;
+            if (st->b_upd == epoch) continue;
+            st->b_upd = epoch;
+            if (st->b_failed) st->b_window = 1;
+            else if (st->b_window) st->b_window *= 2;
+        }
         size_t nnext = 0;
         for (size_t p = 0; p < np; ++p) {
+            if (job_of[p] == SIZE_MAX) { /* held back, in record order */
+                pend[nnext++] = pend[p];
+                continue;
+            }
+            const Job *j = &jobs[job_of[p]];
             if (rc) {
-                if (jobs[p].defer || jobs[p].status == NOISE_ERROR_SYSTEM)
-                    results[jobs[p].idx] = NOISE_ERROR_SYSTEM;
-            } else if (jobs[p].defer) pend[nnext++] = jobs[p].idx;
+                if (j->defer || j->status == NOISE_ERROR_SYSTEM) results[j->idx] = NOISE_ERROR_SYSTEM;
+            } else if (j->defer) {
+                pend[nnext++] = j->idx;
+            }
         }
         np = nnext;
     }
+    if (rc)
+        for (size_t p = 0; p < np; ++p) results[pend[p]] = NOISE_ERROR_SYSTEM;
     free(jobs);
     free(pend);
+    free(job_of);
     return rc;
 }

@@ -48,6 +48,9 @@ typedef struct {
     uint64_t b_epoch;
     uint64_t b_next;   /* nonce the next record of this batch round will use */
     int b_failed;
+    uint64_t b_upd;    /* round whose outcome last set b_window */
+    uint64_t b_window; /* records dispatched per round after a MAC failure (0 = all) */
+    uint64_t b_sent;   /* records dispatched in the current round */
 } HipCipherState;
 
 #define MAX_CHUNKS 64

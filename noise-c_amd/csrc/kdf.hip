@@ -346,8 +346,8 @@ __global__ __launch_bounds__(64) void mix_hash_batch(MixHashArgs a)
 __global__ __launch_bounds__(256) void commit_hash(uint8_t *h, const uint8_t *h_new,
                                                    const uint8_t *status, uint32_t hlen, uint32_t n)
 {
-    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= n * hlen) return;
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (t >= (uint64_t)n * hlen) return;
     if (status[t / hlen] == 0) h[t] = h_new[t];
 }
 

@@ -376,6 +376,14 @@ static int wire_run(int mode, NoiseCipherState *sa, NoiseCipherState *sb, uint8_
         (void)hipStreamSynchronize(sg->stream_out);
         if (!pinned) explicit_bzero(sg->h + wire_base, wire_bytes);
     }
+    if (d_wire && mode != W_SEAL) {
+        /* the device image holds the plaintext of every frame that verified
+           (echo re-seals only the released prefix): zero it once the last
+           D2H has read it, as the host staging is scrubbed above */
+        (void)hipStreamSynchronize(sg->stream_out);
+        if (hipMemsetAsync(d_wire, 0, wire_bytes, sg->stream) == hipSuccess)
+            (void)hipStreamSynchronize(sg->stream);
+    }
     /* nonces: seal advances once per dispatched frame even on a backend error
        (cipherstate.c:325-326); open/echo only for frames that verified */
     if (mode == W_SEAL) {

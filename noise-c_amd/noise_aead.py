@@ -141,6 +141,10 @@ def lib() -> C.CDLL:
         "noise_aead_dev_seal_ragged": (i, [i, P(NoiseAeadRagged), vp]),
         "noise_aead_dev_open_ragged": (i, [i, P(NoiseAeadRagged), vp]),
         "noise_aead_dev_default_lanes": (i, [i, C.c_uint32]),
+        "noise_strerror": (i, [i, C.c_char_p, sz]),
+        "noise_perror": (None, [C.c_char_p, i]),
+        "noise_aead_debug_batch_stats": (None, [P(C.c_uint64), P(C.c_uint64)]),
+        "noise_aead_debug_last_freed_ctx": (vp, [P(sz)]),
         "noise_aead_dev_fill_splitmix": (i, [vp, C.c_uint64, C.c_uint64, C.c_uint64, vp]),
     }
     for name, (res, args) in sigs.items():

@@ -216,3 +216,75 @@ def test_device_api_argument_rules(aead_built):
             assert A.dev_ragged(open_, cid, **{**rg, "out": 0}) == A.ERROR_INVALID_PARAM
         assert A.dev_ragged(open_, A.CHACHAPOLY, **{**rg, "lanes": 5}) == A.ERROR_INVALID_PARAM
         assert A.dev_ragged(open_, 0x4399, **rg) == A.ERROR_UNKNOWN_ID
+
+
+STRERROR = {0: "No error", 0x4501: "Out of memory", 0x4502: "Unknown identifier",
+            0x4503: "Unknown name", 0x4504: "MAC failure", 0x4505: "Not applicable",
+            0x4506: "System error", 0x4507: "Remote public key required",
+            0x4508: "Local keypair required", 0x4509: "Pre shared key required",
+            0x450A: "Invalid length", 0x450B: "Invalid parameter", 0x450C: "Invalid state",
+            0x450D: "Invalid nonce", 0x450E: "Invalid private key", 0x450F: "Invalid public key",
+            0x4510: "Invalid format", 0x4511: "Invalid signature"}
+
+
+def _strerror(lib, err, size=64):
+    buf = C.create_string_buffer(size)
+    rc = lib.noise_strerror(err, buf, size)
+    return rc, buf.value.decode()
+
+
+def test_strerror_contract(L):
+    """noise_strerror / noise_perror of the standalone library: the strings of
+    src/protocol/errors.c:45-63, unknown codes, truncation, bad buffers."""
+    for code, text in STRERROR.items():
+        assert _strerror(L, code) == (0, text)
+    for code in (0x4500, 0x4512, 0x4301, -1, 12345):
+        assert _strerror(L, code) == (0, f"Unknown error 0x{code & 0xffffffff:x}")
+    assert _strerror(L, 0x4504, 4) == (0, "MAC")  # truncated, NUL-terminated
+    assert L.noise_strerror(0x4504, None, 16) == -1
+    buf = C.create_string_buffer(4)
+    assert L.noise_strerror(0x4504, buf, 0) == -1
+    # noise_perror writes "<s>: <text>" to stderr
+    code = ("import sys; sys.path.insert(0, %r); import noise_aead as A; "
+            "A.lib().noise_perror(b'ctx', 0x450D); A.lib().noise_perror(None, 0x4599)"
+            % os.path.join(ROOT, "noise-c_amd"))
+    r = subprocess.run([os.sys.executable, "-c", code], capture_output=True, text=True, check=True)
+    assert r.stderr.splitlines()[-2:] == ["ctx: Invalid nonce", "(null): Unknown error 0x4599"]
+
+
+def test_strerror_matches_reference(L):
+    """The same strings as the reference's own noise_strerror (compiled from
+    /root/reference; build container only)."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "libnoiseref.so")
+    if not os.path.exists(ref):
+        pytest.skip("oracle/_ref not built")
+    R = C.CDLL(ref)
+    R.noise_strerror.argtypes = [C.c_int, C.c_char_p, C.c_size_t]
+    for code in list(STRERROR) + [0x4500, 0x4512, 7]:
+        for size in (64, 5):
+            a, b = C.create_string_buffer(size), C.create_string_buffer(size)
+            assert R.noise_strerror(code, a, size) == L.noise_strerror(code, b, size)
+            assert a.value == b.value, hex(code)
+
+
+def test_ad_longer_than_descriptor_field_refused(aead_built):
+    """AD over 4 GiB cannot be described to the device (32-bit ad_len): the
+    keyed encrypt/decrypt refuse it with INVALID_LENGTH before any GPU work
+    (and leave n alone); a keyless pass-through does not look at AD."""
+    A = aead_built
+    L = A.lib()
+    st = C.c_void_p()
+    assert L.noise_cipherstate_new_by_id(C.byref(st), A.CHACHAPOLY) == 0
+    data = (C.c_uint8 * 64)()
+    ad = (C.c_uint8 * 1)()
+    buf = A.NoiseBuffer(C.cast(data, C.c_void_p), 16, 64)
+    # no key: pass-through, AD ignored
+    assert L.noise_cipherstate_encrypt_with_ad(st, ad, 2**32, C.byref(buf)) == 0
+    key = (C.c_uint8 * 32)(*range(32))
+    assert L.noise_cipherstate_init_key(st, key, 32) == 0
+    assert L.noise_cipherstate_encrypt_with_ad(st, ad, 2**32, C.byref(buf)) == A.ERROR_INVALID_LENGTH
+    buf2 = A.NoiseBuffer(C.cast(data, C.c_void_p), 32, 64)
+    assert L.noise_cipherstate_decrypt_with_ad(st, ad, 2**32 + 5, C.byref(buf2)) == A.ERROR_INVALID_LENGTH
+    n = C.c_uint64()
+    assert L.noise_cipherstate_set_nonce(st, 0) == 0  # n is still 0
+    assert L.noise_cipherstate_free(st) == 0

@@ -1,0 +1,161 @@
+"""GPU tests of the round-2 hardening:
+
+- ragged descriptors longer than NOISE_MAX_PAYLOAD_LEN - 16 are refused
+  (status 2, nothing written), seal and open, both ciphers;
+- a freed CipherState's device key context reads back as zeros (debug hook:
+  NOISE_AEAD_DEBUG_KEEP_FREED keeps the scrubbed allocation alive);
+- a run of forged records in noise_cipherstate_decrypt_batch costs small
+  rounds, not a re-dispatch of everything after each failure, and the results
+  still equal the sequential calls (cipherstate.c:373-410);
+- a state used on two devices is rebuilt on the second (needs 2 GPUs).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CHACHA, AES = 0x4301, 0x4302
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _hip_d2h(ptr, nbytes):
+    """hipMemcpy device -> host through the HIP runtime torch already loaded."""
+    hip = C.CDLL("libamdhip64.so", mode=C.RTLD_GLOBAL)
+    out = (C.c_uint8 * nbytes)()
+    assert hip.hipMemcpy(out, C.c_void_p(ptr), C.c_size_t(nbytes), 2) == 0
+    return bytes(out)
+
+
+@pytest.mark.parametrize("cipher,lanes", [(CHACHA, 4), (CHACHA, 0), (AES, 0), (AES, 4)])
+def test_ragged_refuses_overlong_records(aead, gpu, oracle, cipher, lanes):
+    torch = _torch()
+    sp = torch.cuda.current_stream().cuda_stream
+    rng = np.random.default_rng(77 + lanes + (cipher & 3))
+    key = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    d_key = torch.tensor(list(key), dtype=torch.uint8, device="cuda")
+    ctx = torch.empty(aead.dev_ctx_bytes(cipher), dtype=torch.uint8, device="cuda")
+    assert aead.dev_prepare(cipher, d_key.data_ptr(), 1, ctx.data_ptr(), sp) == 0
+    lens = [100, 65520, 200, 0x1000000 + 5, 65519]
+    slot = 65536 + 64
+    pt = rng.integers(0, 256, len(lens) * slot, dtype=np.uint8)
+    rec_dt = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "<u8"),
+                       ("ad_off", "<u8"), ("len", "<u4"), ("ad_len", "<u4")])
+    recs = np.zeros(len(lens), dtype=rec_dt)
+    recs["in_off"] = recs["out_off"] = np.arange(len(lens)) * slot
+    recs["nonce"] = np.arange(len(lens)) + 7
+    recs["len"] = lens
+    d_recs = torch.from_numpy(recs.view(np.uint8)).to("cuda")
+    d_pt = torch.from_numpy(pt).to("cuda")
+    d_ct = torch.full((len(lens) * slot,), 0xA5, dtype=torch.uint8, device="cuda")
+    st = torch.full((len(lens),), 9, dtype=torch.uint8, device="cuda")
+    kw = dict(ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(), n_records=len(lens), lanes=lanes,
+              flags=aead.FLAG_FAST, stream=sp)
+    assert aead.dev_ragged(False, cipher, inp=d_pt.data_ptr(), out=d_ct.data_ptr(),
+                           status=st.data_ptr(), **kw) == 0
+    torch.cuda.synchronize()
+    ct, s = d_ct.cpu().numpy(), st.cpu().numpy()
+    for i, L in enumerate(lens):
+        seg = ct[i * slot:(i + 1) * slot]
+        if L > 65519:
+            assert s[i] == 2 and np.all(seg == 0xA5), f"len {L} not refused"
+        else:
+            assert s[i] == 0
+            exp = oracle.encrypt(cipher, key, 7 + i, bytes(pt[i * slot:i * slot + L]))
+            assert bytes(seg[:L + 16]) == exp, f"len {L}"
+    # open the sealed records back; the overlong descriptors are refused again
+    d_back = torch.full((len(lens) * slot,), 0x3C, dtype=torch.uint8, device="cuda")
+    st.fill_(9)
+    assert aead.dev_ragged(True, cipher, inp=d_ct.data_ptr(), out=d_back.data_ptr(),
+                           status=st.data_ptr(), **kw) == 0
+    torch.cuda.synchronize()
+    back, s = d_back.cpu().numpy(), st.cpu().numpy()
+    for i, L in enumerate(lens):
+        seg = back[i * slot:(i + 1) * slot]
+        if L > 65519:
+            assert s[i] == 2 and np.all(seg == 0x3C)
+        else:
+            assert s[i] == 0 and np.array_equal(seg[:L], pt[i * slot:i * slot + L])
+
+
+@pytest.mark.parametrize("cipher", [CHACHA, AES])
+def test_freed_state_context_is_scrubbed(aead, gpu, cipher, monkeypatch):
+    """hip_destroy zeroes the device key context (round keys, GHASH tables or
+    the raw ChaCha key) before releasing it (util.c:152-158)."""
+    monkeypatch.setenv("NOISE_AEAD_DEBUG_KEEP_FREED", "1")
+    st = aead.CipherState.new_by_id(cipher)[1]
+    assert st.init_key(bytes(range(1, 33))) == 0
+    ct = st.seal(b"x" * 100)  # builds the device context
+    assert len(ct) == 116
+    assert st.free() == 0
+    n = C.c_size_t()
+    ptr = aead.lib().noise_aead_debug_last_freed_ctx(C.byref(n))
+    assert ptr and n.value == aead.dev_ctx_bytes(cipher)
+    assert _hip_d2h(ptr, n.value) == bytes(n.value), "key context not zeroed"
+
+
+@pytest.mark.parametrize("cipher", [CHACHA, AES])
+def test_forged_run_costs_rounds_not_redispatch(aead, gpu, oracle, cipher):
+    """A state whose batch holds a long run of forged records: results equal
+    the sequential calls, and the records dispatched over all rounds stay
+    linear in the batch (the first version re-ran every later
+    record of the state after each failure, O(n^2))."""
+    rng = np.random.default_rng(5 + (cipher & 3))
+    key = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+    good_before, forged, good_after = 3, 60, 80
+    records, expect_pt = [], []
+    n = 0
+    for i in range(good_before + forged + good_after):
+        L = int(rng.integers(0, 300))
+        pt = bytes(rng.integers(0, 256, L, dtype=np.uint8))
+        if good_before <= i < good_before + forged:
+            records.append(bytes(rng.integers(0, 256, L + 16, dtype=np.uint8)))  # garbage
+            expect_pt.append(None)
+        else:
+            records.append(oracle.encrypt(cipher, key, n, pt))
+            expect_pt.append(pt)
+            n += 1
+    st = aead.CipherState.new_by_id(cipher)[1]
+    st.init_key(key)
+    mems = [(C.c_uint8 * len(r)).from_buffer_copy(r) for r in records]
+    bufs = [aead.NoiseBuffer.input(m, len(r)) for m, r in zip(mems, records)]
+    rc, res = aead.decrypt_batch([st] * len(records), bufs)
+    assert rc == 0
+    for i, exp in enumerate(expect_pt):
+        if exp is None:
+            assert res[i] == 0x4504 and bytes(mems[i]) == records[i], i
+        else:
+            assert res[i] == 0 and bytes(mems[i])[:len(exp)] == exp and bufs[i].size == len(exp), i
+    assert st.nonce == n
+    rounds, disp = C.c_uint64(), C.c_uint64()
+    aead.lib().noise_aead_debug_batch_stats(C.byref(rounds), C.byref(disp))
+    total = len(records)
+    assert disp.value <= 3 * total, (rounds.value, disp.value)
+    assert rounds.value <= forged + 2 + int(np.log2(total)) + 2, (rounds.value, disp.value)
+    st.free()
+
+
+def test_state_moves_between_devices(aead, gpu, oracle):
+    """a state keyed and used on device 0, then used from device 1,
+    gets a context built on device 1 (never device 0's pointer in a device-1
+    kernel); the ciphertexts match the oracle on both."""
+    torch = _torch()
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    key = bytes(range(32))
+    st = aead.CipherState.new_by_id(CHACHA)[1]
+    st.init_key(key)
+    torch.cuda.set_device(0)
+    a = st.seal(b"a" * 50)
+    torch.cuda.set_device(1)
+    b = st.seal(b"b" * 50)
+    torch.cuda.set_device(0)
+    assert a == oracle.encrypt(CHACHA, key, 0, b"a" * 50)
+    assert b == oracle.encrypt(CHACHA, key, 1, b"b" * 50)
+    st.free()
