@@ -56,6 +56,8 @@ typedef struct {
 #define NOISE_CIPHER_CATEGORY NOISE_ID('C', 0)
 #define NOISE_CIPHER_CHACHAPOLY NOISE_ID('C', 1)
 #define NOISE_CIPHER_AESGCM NOISE_ID('C', 2)
+#define NOISE_PADDING_ZERO NOISE_ID('G', 1) /* constants.h:123-124 */
+#define NOISE_PADDING_RANDOM NOISE_ID('G', 2)
 #define NOISE_HASH_BLAKE2s NOISE_ID('H', 1) /* constants.h:43-46 */
 #define NOISE_HASH_BLAKE2b NOISE_ID('H', 2)
 #define NOISE_HASH_SHA256 NOISE_ID('H', 3)
@@ -288,6 +290,37 @@ int noise_aead_dev_encrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
                                     const NoiseAeadRagged *job, void *stream);
 int noise_aead_dev_decrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
                                     const NoiseAeadRagged *job, void *stream);
+
+/* ------------------------------------------------ 6. batched padding
+ *
+ * SURVEY.md §8f rank 4.  n calls of noise_randstate_pad(state, payload_i,
+ * orig_lens[i], padded_len, padding_mode) (randstate.c:348-375) in record
+ * order, payload_i = d_payloads + i*stride, so that messages padded to one
+ * length (echo-client -g, echo-client.c:400-410) go through
+ * noise_aead_dev_seal_uniform.  A record with padded_len <= orig_lens[i] is
+ * left alone and does not touch the generator.
+ *  - NOISE_PADDING_ZERO: the padding bytes are zeroed.
+ *  - NOISE_PADDING_RANDOM (and, as in the reference, any unknown mode): the
+ *    bytes of noise_randstate_generate (:263-316) drawn from *d_rand, a device
+ *    copy of the RandState generator (its ChaCha key, 64-bit block counter,
+ *    64-bit IV and reseed budget `left`, randstate.c:47-58), advanced in place
+ *    exactly as the sequential calls advance it (rekeys included).  When a
+ *    call would need a reseed from OS entropy (left too small) the walk stops
+ *    before that record: records from there on are untouched and *d_done
+ *    (optional) = records processed — the caller reseeds and calls again.
+ *  - d_rand == NULL: the padding is zeroed and NOISE_ERROR_INVALID_PARAM is
+ *    returned (the reference's NULL-state rule).
+ * Device pointers, asynchronous on `stream`. */
+typedef struct NoiseRandSnapshot {
+    uint32_t key[8];
+    uint64_t counter;
+    uint64_t iv;
+    uint64_t left;
+} NoiseRandSnapshot;
+
+int noise_aead_dev_pad(NoiseRandSnapshot *d_rand, uint8_t *d_payloads, uint64_t stride,
+                       const uint32_t *d_orig_lens, uint32_t padded_len, uint32_t n,
+                       int padding_mode, uint32_t *d_done, void *stream);
 
 /* ------------------------------------------------ error reports
  * include/noise/protocol/errors.h; src/protocol/errors.c:92-127. */

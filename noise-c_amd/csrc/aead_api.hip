@@ -17,6 +17,7 @@
 #include "chachapoly.hip"
 #include "aesgcm.hip"
 #include "kdf.hip"
+#include "pad.hip"
 
 using namespace na;
 
@@ -343,6 +344,7 @@ __global__ void splitmix_fill(uint8_t *out, uint64_t nbytes, uint64_t seed, uint
 } // namespace
 
 static_assert(sizeof(NoiseAeadRecord) == sizeof(RecDesc), "record descriptor layout");
+static_assert(sizeof(NoiseRandSnapshot) == sizeof(RandSnap), "RandState snapshot layout");
 static_assert(offsetof(NoiseAeadRecord, ctx_off) == offsetof(RecDesc, ctx_off), "layout");
 
 extern "C" {
@@ -512,6 +514,28 @@ int noise_aead_dev_decrypt_and_hash(int cipher_id, int hash_id, uint8_t *d_h,
     }
     (void)hipFreeAsync(h_new, s);
     return rc;
+}
+
+int noise_aead_dev_pad(NoiseRandSnapshot *d_rand, uint8_t *d_payloads, uint64_t stride,
+                       const uint32_t *d_orig_lens, uint32_t padded_len, uint32_t n,
+                       int padding_mode, uint32_t *d_done, void *stream)
+{
+    if (!d_payloads || (n && !d_orig_lens)) return NOISE_ERROR_INVALID_PARAM;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        if (d_done) return hip_rc(hipMemsetAsync(d_done, 0, sizeof(uint32_t), s));
+        return d_rand ? NOISE_ERROR_NONE : NOISE_ERROR_INVALID_PARAM;
+    }
+    if (!d_rand || padding_mode == NOISE_PADDING_ZERO) {
+        /* randstate.c:356-362: without a state the padding is zeroed anyway */
+        hipLaunchKernelGGL(pad_zero, dim3(n < 65535u ? n : 65535u), dim3(256), 0, s, d_payloads,
+                           stride, d_orig_lens, padded_len, n, d_done);
+        const int rc = hip_rc(hipGetLastError());
+        return rc ? rc : (d_rand ? NOISE_ERROR_NONE : NOISE_ERROR_INVALID_PARAM);
+    }
+    hipLaunchKernelGGL(pad_random, dim3(1), dim3(64), 0, s, (RandSnap *)d_rand, d_payloads, stride,
+                       d_orig_lens, padded_len, n, d_done);
+    return hip_rc(hipGetLastError());
 }
 
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)

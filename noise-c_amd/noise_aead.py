@@ -141,6 +141,7 @@ def lib() -> C.CDLL:
         "noise_aead_dev_seal_ragged": (i, [i, P(NoiseAeadRagged), vp]),
         "noise_aead_dev_open_ragged": (i, [i, P(NoiseAeadRagged), vp]),
         "noise_aead_dev_default_lanes": (i, [i, C.c_uint32]),
+        "noise_aead_dev_pad": (i, [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, i, vp, vp]),
         "noise_strerror": (i, [i, C.c_char_p, sz]),
         "noise_perror": (None, [C.c_char_p, i]),
         "noise_aead_debug_batch_stats": (None, [P(C.c_uint64), P(C.c_uint64)]),
@@ -373,6 +374,16 @@ def dev_duplex(cipher: int, seal_job: NoiseAeadUniform, open_job: NoiseAeadUnifo
     """noise_aead_dev_duplex_uniform: seal_job and open_job in one launch."""
     return lib().noise_aead_dev_duplex_uniform(cipher, C.byref(seal_job), C.byref(open_job),
                                                stream or None)
+
+
+PADDING_ZERO, PADDING_RANDOM = NOISE_ID("G", 1), NOISE_ID("G", 2)
+
+
+def dev_pad(*, rand: int, payloads: int, stride: int, orig_lens: int, padded_len: int, n: int,
+            mode: int, done: int = 0, stream: int = 0) -> int:
+    """noise_aead_dev_pad (device pointers; rand may be 0 = NULL state)."""
+    return lib().noise_aead_dev_pad(rand or None, payloads, stride, orig_lens, padded_len, n, mode,
+                                    done or None, stream or None)
 
 
 def dev_ragged(open_: bool, cipher: int, *, ctx_base: int, recs: int, inp: int, out: int,

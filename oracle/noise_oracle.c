@@ -476,3 +476,60 @@ void oracle_fill_splitmix(uint64_t seed, uint64_t word0, uint8_t *out, size_t nb
         memcpy(out + 8 * w, tmp, nbytes - 8 * w);
     }
 }
+
+/* ---------------------------------------------------------------- RandState
+ * randstate.c:230-375 restated over a snapshot (see noise_oracle.h). */
+#define ORACLE_PADDING_ZERO 0x4701 /* constants.h:123 NOISE_PADDING_ZERO */
+
+static void rand_block(const OracleRand *s, uint8_t out[64])
+{
+    uint8_t k[32];
+    for (int i = 0; i < 8; ++i) st32le(k + 4 * i, s->key[i]);
+    oracle_chacha20_block(k, s->counter, s->iv, out);
+}
+
+/* randstate.c:230-247: 40 key-stream bytes at the current position become
+   the new key and IV, counter 0 */
+static void rand_rekey(OracleRand *s)
+{
+    uint8_t b[64];
+    rand_block(s, b);
+    for (int i = 0; i < 8; ++i) s->key[i] = ld32le(b + 4 * i);
+    s->iv = (uint64_t)ld32le(b + 32) | ((uint64_t)ld32le(b + 36) << 32);
+    s->counter = 0;
+    memset(b, 0, sizeof b);
+}
+
+int oracle_rand_pad(OracleRand *s, uint8_t *payload, size_t orig_len, size_t padded_len, int mode)
+{
+    if (!payload) return 0x450B;
+    if (!s) {
+        if (padded_len > orig_len) memset(payload + orig_len, 0, padded_len - orig_len);
+        return 0x450B;
+    }
+    if (padded_len <= orig_len) return 0;
+    const size_t len = padded_len - orig_len;
+    uint8_t *out = payload + orig_len;
+    if (mode == ORACLE_PADDING_ZERO) {
+        memset(out, 0, len);
+        return 0;
+    }
+    /* every 64-byte chunk, the partial last one too, spends 64 of `left` */
+    const size_t chunks = (len + 63) / 64;
+    if (s->left < len || s->left < 64 * chunks) return 0x450C;
+    unsigned blocks = 0;
+    for (size_t c = 0; c < chunks; ++c) {
+        s->left -= 64;
+        if (blocks++ >= 16) { /* NOISE_RAND_REKEY_COUNT */
+            rand_rekey(s);
+            blocks = 0;
+        }
+        uint8_t b[64];
+        rand_block(s, b);
+        ++s->counter;
+        const size_t n = len - 64 * c < 64 ? len - 64 * c : 64;
+        memcpy(out + 64 * c, b, n);
+    }
+    rand_rekey(s);
+    return 0;
+}

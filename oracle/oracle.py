@@ -40,6 +40,21 @@ def _buf(b):
     return (C.c_uint8 * len(b)).from_buffer(b) if len(b) else (C.c_uint8 * 1)()
 
 
+class RandSnapshot(C.Structure):
+    """OracleRand / NoiseRandSnapshot: the RandState generator's ChaCha key,
+    64-bit block counter, 64-bit IV and reseed budget (randstate.c:47-58)."""
+    _fields_ = [("key", C.c_uint32 * 8), ("counter", C.c_uint64), ("iv", C.c_uint64),
+                ("left", C.c_uint64)]
+
+    def copy(self):
+        c = RandSnapshot()
+        C.memmove(C.byref(c), C.byref(self), C.sizeof(self))
+        return c
+
+    def words(self):
+        return (list(self.key), self.counter, self.iv, self.left)
+
+
 class Oracle:
     def __init__(self, path: str = ORACLE_SO):
         if not os.path.exists(path):
@@ -61,6 +76,7 @@ class Oracle:
         L.oracle_fill_splitmix.argtypes = [C.c_uint64, C.c_uint64, u8p, sz]
         L.oracle_hash.argtypes = [C.c_int, u8p, sz, u8p]
         L.oracle_hkdf.argtypes = [C.c_int, u8p, sz, u8p, sz, u8p, sz, u8p, sz]
+        L.oracle_rand_pad.argtypes = [C.c_void_p, u8p, sz, sz, C.c_int]
         self.L = L
 
     @staticmethod
@@ -115,6 +131,12 @@ class Oracle:
         out, xx, hh = bytearray(16), bytearray(x), bytearray(h)
         self.L.oracle_gf128_mul(self._p(xx), self._p(hh), self._p(out))
         return bytes(out)
+
+    def rand_pad(self, snap, payload: bytearray, orig_len: int, padded_len: int, mode: int) -> int:
+        """One noise_randstate_pad call on snapshot `snap` (a RandSnapshot,
+        updated in place, or None) over `payload` (bytearray, in place)."""
+        p = C.byref(snap) if snap is not None else None
+        return self.L.oracle_rand_pad(p, self._p(payload), orig_len, padded_len, mode)
 
     def splitmix64(self, x: int) -> int:
         return self.L.oracle_splitmix64(x)
