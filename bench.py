@@ -248,7 +248,7 @@ def _cpu_baseline(cfg, budget_cpu_s):
     return res
 
 
-def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length, duplex=False):
+def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length, duplex=False, ct=False):
     """The kernel the library dispatches for this uniform job's seal
     (aead_api.hip run_uniform) or, duplex, for the whole step (run_duplex), as
     rocprofv3 names it."""
@@ -256,7 +256,8 @@ def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length, duplex=Fal
     if duplex and cipher == CHACHA and fast and lanes in (4, 8):
         return f"chachapoly_duplex_staged<{lanes}, {'true' if rps % (64 // lanes) == 0 else 'false'}>"
     if cipher == AES:
-        return "gcm_staged<false>" if fast and rps % 256 == 0 else "gcm_uniform<false>"
+        c = "true" if ct else "false"
+        return f"gcm_staged<false, {c}>" if fast and rps % 256 == 0 else f"gcm_uniform<false, {c}>"
     if fast and lanes >= 4:
         return f"chachapoly_seal_staged<{lanes}, {'true' if rps % (64 // lanes) == 0 else 'false'}>"
     return f"chachapoly_seal_uniform<{lanes}, {'true' if fast else 'false'}>"
@@ -317,6 +318,8 @@ def main():
                          "its interval / launches); step: events at every launch boundary")
     ap.add_argument("--streams", type=int, default=1, choices=(1, 2),
                     help="C2-C4/perf: 2 = consecutive steps alternate between two streams")
+    ap.add_argument("--ct-ghash", action="store_true",
+                    help="AES-GCM: NOISE_AEAD_FLAG_CT_GHASH (table-free GHASH)")
     ap.add_argument("--c5-streams", type=int, default=2, choices=(1, 2),
                     help="C5: 2 = the AES-GCM and ChaChaPoly halves on two streams, concurrently")
     args = ap.parse_args()
@@ -382,6 +385,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     lanes = args.lanes or A.dev_default_lanes(cipher, N)
+    jflags = A.FLAG_CT_GHASH if args.ct_ghash else 0
 
     def seal(b, pt=None, ct=None, stream=sp):
         if pt is None:
@@ -389,7 +393,8 @@ def main():
         return A.dev_uniform(False, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
                              inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
                              out_stride=out_stride, length=L, n_records=N,
-                             recs_per_state=sh["rps"], lanes=lanes, stream=stream, **ad_kw)
+                             recs_per_state=sh["rps"], lanes=lanes, flags=jflags, stream=stream,
+                             **ad_kw)
 
     def open_(b, stream=sp):
         _, ct, back, st = sets[b]
@@ -397,7 +402,7 @@ def main():
                              inp=ct.data_ptr(), out=back.data_ptr(), in_stride=out_stride,
                              out_stride=in_stride, length=L, n_records=N,
                              recs_per_state=sh["rps"], status=st.data_ptr(), lanes=lanes,
-                             stream=stream, **ad_kw)
+                             flags=jflags, stream=stream, **ad_kw)
 
     # Each step seals set b = s % sets and opens set (s - LAG) % sets, sealed LAG
     # steps earlier: the ciphertext an open reads was written two full steps
@@ -411,7 +416,7 @@ def main():
         pt, ct, _, _ = sets[b]
         _, cto, back, st = sets[bo]
         common = dict(ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(), length=L, n_records=N,
-                      recs_per_state=sh["rps"], lanes=lanes, **ad_kw)
+                      recs_per_state=sh["rps"], lanes=lanes, flags=jflags, **ad_kw)
         sj = A.uniform_job(inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
                            out_stride=out_stride, **common)
         oj = A.uniform_job(inp=cto.data_ptr(), out=back.data_ptr(), in_stride=out_stride,
@@ -510,7 +515,7 @@ def main():
     payload_step = 2.0 * N * L * world                         # both directions, all ranks
     value = payload_step * args.steps / elapsed / GIB
     alg_seal = N * (2 * L + 16 + AD) + len(sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
-    kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L, duplex)
+    kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L, duplex, args.ct_ghash)
     if kname.startswith("chachapoly_duplex"):
         # the one launch of a step: one seal + one open of N records each
         alg_launch, launch_ms_ = 2 * alg_seal, launch_ms
@@ -544,7 +549,8 @@ def main():
                    "in_stride": in_stride, "out_stride": out_stride,
                    "payload_bytes_per_step": int(payload_step), "parallelism": f"records x{world}",
                    "streams": len(streams), "mode": args.mode, "events": args.events,
-                   "open_reads_set_sealed_steps_before": lag},
+                   "open_reads_set_sealed_steps_before": lag,
+                   **({"ct_ghash": True} if args.ct_ghash else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": kname,
@@ -777,7 +783,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     if g["cipher"] == CHACHA:
         kname = f"chachapoly_{'open' if open_ else 'seal'}_ragged<{args.lanes or 4}, true>"
     else:
-        kname = f"gcm_ragged_staged<{'true' if open_ else 'false'}, true, 1024>"
+        kname = f"gcm_ragged_staged<{'true' if open_ else 'false'}, true, 1024, false>"
     pmc = load_pmc("c5", kname)
     result = {
         "metric": "GiB/s device-resident AEAD encrypt+decrypt, mixed 64B-16KiB records per GPU",

@@ -202,7 +202,7 @@ typedef struct NoiseAeadUniform {
     uint32_t len;            /* <= 65535 - 16 */
     uint32_t ad_len;
     uint32_t lanes_per_record;
-    uint32_t reserved_;
+    uint32_t flags;          /* NOISE_AEAD_FLAG_CT_GHASH (FAST is derived) */
 } NoiseAeadUniform;
 
 int noise_aead_dev_seal_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream);
@@ -254,6 +254,17 @@ typedef struct NoiseAeadRagged {
  * bytes (and holds CT || tag for open).  Enables the straight-line dwordx4 path.  The
  * uniform API derives this itself from the pointers and strides. */
 #define NOISE_AEAD_FLAG_FAST 1u
+
+/* AESGCM only: GHASH without lookup tables.  The default GHASH multiplies
+ * by H through 4-bit tables indexed by the running hash (LDS copies are
+ * bank-conflict-free; the per-lane final scale reads the context's tables in
+ * global memory, whose cache-line footprint depends on secret data).  With
+ * this flag every multiply is a carry-less 128x128 product built from integer
+ * multiplies of masked operands (no secret-dependent address or branch) —
+ * slower; DESIGN.md §4 gives both throughputs.  Setting the environment
+ * variable NOISE_AEAD_CT_GHASH=1 before the first call turns it on for every
+ * job, including the CipherState and wire paths. */
+#define NOISE_AEAD_FLAG_CT_GHASH 2u
 
 int noise_aead_dev_seal_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);
 int noise_aead_dev_open_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);

@@ -187,6 +187,27 @@ UniformArgs to_args(const NoiseAeadUniform *j)
     return a;
 }
 
+/* NOISE_AEAD_FLAG_CT_GHASH, or NOISE_AEAD_CT_GHASH=1 in the environment
+   (read once) for every job */
+bool ct_ghash(uint32_t flags)
+{
+    static const bool env = [] {
+        const char *e = getenv("NOISE_AEAD_CT_GHASH");
+        return e && e[0] == '1';
+    }();
+    return (flags & NOISE_AEAD_FLAG_CT_GHASH) || env;
+}
+
+template <bool CT>
+KernelFn<RaggedArgs> gcm_ragged_fn(bool open, bool fast, bool big)
+{
+    if (big)
+        return open ? (fast ? gcm_ragged_staged<true, true, 1024, CT> : gcm_ragged_staged<true, false, 1024, CT>)
+                    : (fast ? gcm_ragged_staged<false, true, 1024, CT> : gcm_ragged_staged<false, false, 1024, CT>);
+    return open ? (fast ? gcm_ragged_staged<true, true, 256, CT> : gcm_ragged_staged<true, false, 256, CT>)
+                : (fast ? gcm_ragged_staged<false, true, 256, CT> : gcm_ragged_staged<false, false, 256, CT>);
+}
+
 int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool open)
 {
     int rc = check_uniform(job);
@@ -209,16 +230,19 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
             return NOISE_ERROR_INVALID_PARAM;
         rc = hip_rc(ensure_aes_tables(s));
         if (rc) return rc;
+        const bool ct = ct_ghash(job->flags);
         /* one state per 256-record workgroup + FAST layout -> LDS-staged kernel */
         if (uniform_fast(job, open) && job->recs_per_state % GCM_WG_RECS == 0) {
             if (job->n_records == 0) return NOISE_ERROR_NONE;
             const uint32_t blocks = (job->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
-            hipLaunchKernelGGL(open ? gcm_staged<true> : gcm_staged<false>, dim3(blocks),
-                               dim3(GCM_WG), 0, s, a);
+            hipLaunchKernelGGL(ct ? (open ? gcm_staged<true, true> : gcm_staged<false, true>)
+                                  : (open ? gcm_staged<true, false> : gcm_staged<false, false>),
+                               dim3(blocks), dim3(GCM_WG), 0, s, a);
             return hip_rc(hipGetLastError());
         }
-        return launch(open ? gcm_uniform<true> : gcm_uniform<false>, job->n_records,
-                      GCM_LANES, a, s);
+        return launch(ct ? (open ? gcm_uniform<true, true> : gcm_uniform<false, true>)
+                         : (open ? gcm_uniform<true, false> : gcm_uniform<false, false>),
+                      job->n_records, GCM_LANES, a, s);
     }
     return NOISE_ERROR_UNKNOWN_ID;
 }
@@ -297,27 +321,24 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
         int rc = hip_rc(ensure_aes_tables(s));
         if (rc) return rc;
         if (job->n_records == 0) return NOISE_ERROR_NONE;
+        const bool ct = ct_ghash(job->flags);
         /* LDS-staged kernel: 1024-thread workgroups over 256-record windows;
            a batch too small to give every CU one of those uses 256-thread
            workgroups over 64-record windows instead (4x the workgroups) */
         if (job->lanes_per_record == 0 && job->n_records <= WIDE_MAX_RECORDS) {
             /* small batch: a workgroup per record (latency, not throughput);
                lanes_per_record = 4 keeps the windowed 4-lane kernels */
-            hipLaunchKernelGGL(open ? gcm_wide<true> : gcm_wide<false>, dim3(job->n_records),
-                               dim3(256), 0, s, a);
+            hipLaunchKernelGGL(ct ? (open ? gcm_wide<true, true> : gcm_wide<false, true>)
+                                  : (open ? gcm_wide<true, false> : gcm_wide<false, false>),
+                               dim3(job->n_records), dim3(256), 0, s, a);
             return hip_rc(hipGetLastError());
         }
         const bool fast = (job->flags & NOISE_AEAD_FLAG_FAST) != 0;
         const bool big = job->n_records >= 256u * GCM_WG_RECS;
         const uint32_t per = big ? GCM_WG_RECS : GCM_WG_RECS / 4;
         const uint32_t blocks = (job->n_records + per - 1) / per;
-        KernelFn<RaggedArgs> fn;
-        if (big)
-            fn = open ? (fast ? gcm_ragged_staged<true, true, 1024> : gcm_ragged_staged<true, false, 1024>)
-                      : (fast ? gcm_ragged_staged<false, true, 1024> : gcm_ragged_staged<false, false, 1024>);
-        else
-            fn = open ? (fast ? gcm_ragged_staged<true, true, 256> : gcm_ragged_staged<true, false, 256>)
-                      : (fast ? gcm_ragged_staged<false, true, 256> : gcm_ragged_staged<false, false, 256>);
+        KernelFn<RaggedArgs> fn = ct ? gcm_ragged_fn<true>(open, fast, big)
+                                     : gcm_ragged_fn<false>(open, fast, big);
         hipLaunchKernelGGL(fn, dim3(blocks), dim3(big ? 1024 : 256), 0, s, a);
         return hip_rc(hipGetLastError());
     }

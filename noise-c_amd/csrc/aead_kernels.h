@@ -111,6 +111,8 @@ struct AesCtx {
     uint32_t pad_[12];
     /* tab[m]: multiply-by-H^(m+1) tables, m = 0..3 (H^4 is the Horner step) */
     uint32_t tab[GCM_LANES][GHASH_TAB_ENTRIES][4];
+    /* hn[m]: H^(m+1) in the natural polynomial domain (constant-time GHASH) */
+    uint32_t hn[GCM_LANES][4];
 };
 
 } // namespace na

@@ -120,6 +120,85 @@ NA_DEV void gh_mul(uint32_t y[4], const uint4 *__restrict__ tab)
 
 NA_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 
+/* ------------------------------------------- constant-time GHASH (opt-in)
+ *
+ * NOISE_AEAD_FLAG_CT_GHASH: the GHASH multiplies touch no table — the
+ * property the reference's bit-serial GF128_mul has (ghash.c:85-108).  The
+ * field element is held in the natural polynomial domain (bit i of the
+ * 128-bit word vector = coefficient of x^i): a GCM block loaded as LE words
+ * maps there by reversing the bits of each byte (bswap . bfrev, its own
+ * inverse).  The product is a carry-less 128x128 multiply — two levels of
+ * Karatsuba over nine 32x32 products — reduced by x^128 + x^7 + x^2 + x + 1.
+ * A 32x32 carry-less product comes from integer multiplies: split each
+ * operand into four parts holding every 4th bit; an integer product of two
+ * parts has at most 8 terms on any bit position of its class, so the carries
+ * stay in the three positions above it, which the class mask drops (the
+ * BearSSL "ctmul" construction).  ≈ 620 VALU per block multiply, no LDS. */
+NA_DEV uint32_t gh_nat(uint32_t w) { return __builtin_bswap32(__builtin_bitreverse32(w)); }
+
+NA_DEV uint64_t clmul32(uint32_t a, uint32_t b)
+{
+    const uint32_t a0 = a & 0x11111111u, a1 = a & 0x22222222u, a2 = a & 0x44444444u,
+                   a3 = a & 0x88888888u;
+    const uint32_t b0 = b & 0x11111111u, b1 = b & 0x22222222u, b2 = b & 0x44444444u,
+                   b3 = b & 0x88888888u;
+    const uint64_t z0 = ((uint64_t)a0 * b0) ^ ((uint64_t)a1 * b3) ^ ((uint64_t)a2 * b2) ^ ((uint64_t)a3 * b1);
+    const uint64_t z1 = ((uint64_t)a0 * b1) ^ ((uint64_t)a1 * b0) ^ ((uint64_t)a2 * b3) ^ ((uint64_t)a3 * b2);
+    const uint64_t z2 = ((uint64_t)a0 * b2) ^ ((uint64_t)a1 * b1) ^ ((uint64_t)a2 * b0) ^ ((uint64_t)a3 * b3);
+    const uint64_t z3 = ((uint64_t)a0 * b3) ^ ((uint64_t)a1 * b2) ^ ((uint64_t)a2 * b1) ^ ((uint64_t)a3 * b0);
+    return (z0 & 0x1111111111111111ull) | (z1 & 0x2222222222222222ull) |
+           (z2 & 0x4444444444444444ull) | (z3 & 0x8888888888888888ull);
+}
+
+/* 64x64 -> 128 carry-less (Karatsuba): r[0..3] */
+NA_DEV void clmul64(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1, uint32_t r[4])
+{
+    const uint64_t lo = clmul32(a0, b0), hi = clmul32(a1, b1);
+    const uint64_t mid = clmul32(a0 ^ a1, b0 ^ b1) ^ lo ^ hi;
+    r[0] = (uint32_t)lo;
+    r[1] = (uint32_t)(lo >> 32) ^ (uint32_t)mid;
+    r[2] = (uint32_t)hi ^ (uint32_t)(mid >> 32);
+    r[3] = (uint32_t)(hi >> 32);
+}
+
+/* y <- y * h in GF(2^128), both in the natural domain */
+NA_DEV void gh_mul_ct(uint32_t y[4], const uint32_t h[4])
+{
+    uint32_t lo[4], hi[4], mid[4];
+    clmul64(y[0], y[1], h[0], h[1], lo);
+    clmul64(y[2], y[3], h[2], h[3], hi);
+    clmul64(y[0] ^ y[2], y[1] ^ y[3], h[0] ^ h[2], h[1] ^ h[3], mid);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mid[i] = xor3(mid[i], lo[i], hi[i]);
+    /* P = hi x^128 + mid x^64 + lo: 256-bit words p0..p7 */
+    const uint32_t p0 = lo[0], p1 = lo[1], p2 = lo[2] ^ mid[0], p3 = lo[3] ^ mid[1];
+    const uint32_t p4 = hi[0] ^ mid[2], p5 = hi[1] ^ mid[3], p6 = hi[2], p7 = hi[3];
+    /* p4..p7 x^128 = (p4..p7)(x^7 + x^2 + x + 1): shift-XOR, then fold the
+       bits shifted past x^127 (degree <= 6) the same way */
+    const uint32_t t0 = xor3(p4, p4 << 1, p4 << 2) ^ (p4 << 7);
+    const uint32_t t1 = xor3(p5, __builtin_amdgcn_alignbit(p5, p4, 31), __builtin_amdgcn_alignbit(p5, p4, 30)) ^
+                        __builtin_amdgcn_alignbit(p5, p4, 25);
+    const uint32_t t2 = xor3(p6, __builtin_amdgcn_alignbit(p6, p5, 31), __builtin_amdgcn_alignbit(p6, p5, 30)) ^
+                        __builtin_amdgcn_alignbit(p6, p5, 25);
+    const uint32_t t3 = xor3(p7, __builtin_amdgcn_alignbit(p7, p6, 31), __builtin_amdgcn_alignbit(p7, p6, 30)) ^
+                        __builtin_amdgcn_alignbit(p7, p6, 25);
+    const uint32_t o = xor3(p7 >> 31, p7 >> 30, p7 >> 25);
+    const uint32_t f = xor3(o, o << 1, o << 2) ^ (o << 7);
+    y[0] = xor3(p0, t0, f);
+    y[1] = p1 ^ t1;
+    y[2] = p2 ^ t2;
+    y[3] = p3 ^ t3;
+}
+
+/* GCM-domain LE words <-> natural domain (the map is an involution) */
+NA_DEV void gh_to_nat(uint32_t x[4])
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = gh_nat(x[i]);
+}
+
+
+
 /* gh_mul with the table in LDS: lookups taken in pairs so every accumulate is
    one 3-input XOR */
 template <bool THROTTLE = false>
@@ -139,6 +218,29 @@ NA_DEV void gh_mul_lds(uint32_t y[4], const uint4 *tab)
         if (THROTTLE && (p & 6) == 6) asm volatile("" ::: "memory");
     }
     y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
+}
+
+/* The Horner step y <- y * H^4 (tables in LDS, or constant-time: y and the
+   blocks in the natural domain, hn4 = H^4 there) and the final scale
+   y <- y * H^(m+1) (the context's tables in global memory, or CT). */
+template <bool CT, bool THROTTLE = false>
+NA_DEV void gh_step(uint32_t y[4], const uint4 *tab_lds, const uint32_t hn4[4])
+{
+    if constexpr (CT) gh_mul_ct(y, hn4);
+    else gh_mul_lds<THROTTLE>(y, tab_lds);
+}
+
+template <bool CT>
+NA_DEV void gh_scale(uint32_t y[4], const AesCtx *ctx, int m)
+{
+    if constexpr (CT) {
+        uint32_t h[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) h[w] = ctx->hn[m][w];
+        gh_mul_ct(y, h);
+    } else {
+        gh_mul(y, (const uint4 *)ctx->tab[m]);
+    }
 }
 
 /* ----------------------------------------------------------- key prepare */
@@ -220,6 +322,12 @@ __global__ __launch_bounds__(256) void gcm_prepare(const uint8_t *__restrict__ r
         for (int j = 0; j < 4; ++j) w |= (uint32_t)hp[0][4 * t + j] << (8 * j);
         c->h[t] = w;
     }
+    if (t < 4 * GCM_LANES) { /* H^1..H^4, natural domain */
+        const int m = t >> 2, q = t & 3;
+        uint32_t w = 0;
+        for (int j = 0; j < 4; ++j) w |= (uint32_t)hp[m][4 * q + j] << (8 * j);
+        c->hn[m][q] = gh_nat(w);
+    }
     for (int e = t; e < GCM_LANES * GHASH_TAB_ENTRIES; e += 256) {
         const int m = e / GHASH_TAB_ENTRIES, p = (e / 16) % 32, val = e % 16;
         uint8_t acc[16] = {0};
@@ -245,7 +353,7 @@ struct GcmView {
 };
 
 /* Returns (seal) true; (open) whether the tag verified. */
-template <bool OPEN>
+template <bool OPEN, bool CT>
 NA_DEV bool gcm_record(const GcmView &rv, int l, const uint32_t *te, const uint32_t *sb)
 {
     constexpr int K = GCM_LANES;
@@ -255,9 +363,17 @@ NA_DEV bool gcm_record(const GcmView &rv, int l, const uint32_t *te, const uint3
     const uint32_t n = A + M + 1;
     const uint32_t c0 = ((uint32_t)l + n) % K;
     const uint4 *tabH4 = (const uint4 *)ctx->tab[K - 1];
+    uint32_t h4n[4] = {0, 0, 0, 0};
+    if constexpr (CT) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) h4n[w] = ctx->hn[K - 1][w];
+    }
     uint32_t acc[4] = {0, 0, 0, 0};
     for (uint32_t i = c0; i < n; i += K) {
-        if (i != c0) gh_mul(acc, tabH4);
+        if (i != c0) {
+            if constexpr (CT) gh_mul_ct(acc, h4n);
+            else gh_mul(acc, tabH4);
+        }
         uint32_t x[4];
         if (i < A) {
             const uint32_t rem = rv.ad_len - 16 * i;
@@ -283,14 +399,16 @@ NA_DEV bool gcm_record(const GcmView &rv, int l, const uint32_t *te, const uint3
             x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
             x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
         }
+        if constexpr (CT) gh_to_nat(x);
         acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
     }
     /* scale by H^(K-l) (lane l's last block has exponent K-l) */
-    gh_mul(acc, (const uint4 *)ctx->tab[K - 1 - l]);
+    gh_scale<CT>(acc, ctx, K - 1 - l);
 #pragma unroll
     for (int off = 1; off < K; off <<= 1)
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+    if constexpr (CT) gh_to_nat(acc); /* back to the GCM domain */
     /* tag = E_K(J0) xor S: every lane of the group computes it (one AES) */
     uint32_t ej[4];
     aes_ctr_block(rk, te, sb, rv.nonce, 1u, ej);
@@ -325,7 +443,7 @@ NA_DEV void load_aes_tables(uint32_t *te, uint32_t *sb)
     __syncthreads();
 }
 
-template <bool OPEN>
+template <bool OPEN, bool CT>
 __global__ __launch_bounds__(256) void gcm_uniform(UniformArgs a)
 {
     __shared__ uint32_t te[256], sb[256];
@@ -343,11 +461,11 @@ __global__ __launch_bounds__(256) void gcm_uniform(UniformArgs a)
     rv.nonce = a.nonce_base[st] + (uint64_t)(rec - st * a.rps);
     rv.len = a.len;
     rv.ad_len = a.ad_len;
-    const bool ok = gcm_record<OPEN>(rv, l, te, sb);
+    const bool ok = gcm_record<OPEN, CT>(rv, l, te, sb);
     if (OPEN && l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
-template <bool OPEN>
+template <bool OPEN, bool CT>
 __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
 {
     __shared__ uint32_t te[256], sb[256];
@@ -368,7 +486,7 @@ __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
     rv.nonce = d.nonce;
     rv.len = d.len;
     rv.ad_len = d.ad_len;
-    const bool ok = gcm_record<OPEN>(rv, l, te, sb);
+    const bool ok = gcm_record<OPEN, CT>(rv, l, te, sb);
     if (l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
@@ -540,7 +658,7 @@ NA_DEV uint32_t blk_mask(uint32_t nb, int w)
     return rb >= 4 ? 0xffffffffu : (rb <= 0 ? 0u : ((1u << (8 * rb)) - 1u));
 }
 
-template <bool OPEN>
+template <bool OPEN, bool CT>
 __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
 {
     constexpr int K = GCM_LANES;
@@ -568,12 +686,17 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
     const uint32_t c0 = ((uint32_t)l + n) % K;
 
     /* GHASH (and, sealing, CTR) over this lane's blocks i = c0, c0+K, ... */
+    uint32_t h4n[4] = {0, 0, 0, 0};
+    if constexpr (CT) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) h4n[w] = ctx->hn[K - 1][w];
+    }
     uint32_t acc[4] = {0, 0, 0, 0};
     AesPre pre;
     if (!OPEN) pre = aes_pre_lds(TE, L.rk, tpl, n_hi, n_lo);
 #pragma unroll 1
     for (uint32_t i = c0; i < n; i += K) {
-        if (i != c0) gh_mul_lds<OPEN>(acc, L.h4);
+        if (i != c0) gh_step<CT, OPEN>(acc, L.h4, h4n);
         uint32_t x[4];
         if (i >= A && i < A + M) {
             const uint32_t d = i - A;
@@ -598,14 +721,16 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
             x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
             x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
         }
+        if constexpr (CT) gh_to_nat(x);
         acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
     }
     /* scale by H^(K-l) from the context's tables (once per lane) */
-    gh_mul(acc, (const uint4 *)ctx->tab[K - 1 - l]);
+    gh_scale<CT>(acc, ctx, K - 1 - l);
 #pragma unroll
     for (int off = 1; off < K; off <<= 1)
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+    if constexpr (CT) gh_to_nat(acc);
     if (OPEN) pre = aes_pre_lds(TE, L.rk, tpl, n_hi, n_lo);
     uint32_t ej[4];
     aes_ctr_pre(TE, L.rk, tpl, pre, 1u, ej);
@@ -659,11 +784,16 @@ struct GcmLdsR {
 /* One record, 4 lanes (l = 0..3): gcm_staged's GHASH/CTR core with the
    record's tables passed in; FAST as in chachapoly.hip (16-B aligned record,
    input readable to roundup16). */
-template <bool OPEN, bool FAST>
+template <bool OPEN, bool FAST, bool CT>
 NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint32_t tpl,
                               const uint32_t *rk, const uint4 *h4)
 {
     constexpr int K = GCM_LANES;
+    uint32_t h4n[4] = {0, 0, 0, 0};
+    if constexpr (CT) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) h4n[w] = rv.ctx->hn[K - 1][w];
+    }
     const uint32_t n_hi = (uint32_t)(rv.nonce >> 32), n_lo = (uint32_t)rv.nonce;
     const uint32_t len = rv.len, ad_len = rv.ad_len;
     const uint32_t A = (ad_len + 15) / 16, M = (len + 15) / 16;
@@ -674,7 +804,7 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
     if (!OPEN) pre = aes_pre_lds(TE, rk, tpl, n_hi, n_lo);
 #pragma unroll 1
     for (uint32_t i = c0; i < n; i += K) {
-        if (i != c0) gh_mul_lds<OPEN>(acc, h4);
+        if (i != c0) gh_step<CT, OPEN>(acc, h4, h4n);
         uint32_t x[4];
         if (i >= A && i < A + M) {
             const uint32_t d = i - A;
@@ -703,13 +833,15 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
             x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
             x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
         }
+        if constexpr (CT) gh_to_nat(x);
         acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
     }
-    gh_mul(acc, (const uint4 *)rv.ctx->tab[K - 1 - l]);
+    gh_scale<CT>(acc, rv.ctx, K - 1 - l);
 #pragma unroll
     for (int off = 1; off < K; off <<= 1)
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+    if constexpr (CT) gh_to_nat(acc);
     if (OPEN) pre = aes_pre_lds(TE, rk, tpl, n_hi, n_lo);
     uint32_t ej[4];
     aes_ctr_pre(TE, rk, tpl, pre, 1u, ej);
@@ -744,17 +876,17 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
    out-of-line call its frame and caller-saved registers cost the slot path
    scratch traffic (open 176 -> 104 B/lane, seal 64 -> 0) and C5's AES
    kernels 2-5 % (profiles/r01_aes_inline_ab.jsonl). */
-template <bool OPEN, bool FAST>
+template <bool OPEN, bool FAST, bool CT>
 __device__ __forceinline__ bool gcm_record_global(const GcmView &rv, int l,
                                                   const uint8_t *TE, uint32_t tpl)
 {
-    return gcm_record_staged<OPEN, FAST>(rv, l, TE, tpl, rv.ctx->rk,
-                                         (const uint4 *)rv.ctx->tab[GCM_LANES - 1]);
+    return gcm_record_staged<OPEN, FAST, CT>(rv, l, TE, tpl, rv.ctx->rk,
+                                             (const uint4 *)rv.ctx->tab[GCM_LANES - 1]);
 }
 
 /* WG threads per workgroup (1024, or 256 for batches too small to give
    every CU a 1024-thread workgroup); WG / 4 records per window */
-template <bool OPEN, bool FAST, int WG>
+template <bool OPEN, bool FAST, int WG, bool CT>
 __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
 {
     constexpr int K = GCM_LANES, NREC = WG / GCM_LANES;
@@ -774,7 +906,8 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
     for (int sl = 0; sl < 2; ++sl) {
         const AesCtx *ctx = (const AesCtx *)(a.keys + slot_off[sl]);
         const uint4 *src = (const uint4 *)ctx->tab[K - 1];
-        for (int i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += WG) L.h4[sl][i] = src[i];
+        if (!CT)
+            for (int i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += WG) L.h4[sl][i] = src[i];
         if (threadIdx.x < 60) L.rk[sl][threadIdx.x] = ctx->rk[threadIdx.x];
     }
     const uint32_t rec = window_rec<NREC>(a.recs, a.n_records, base, threadIdx.x / K, L.order);
@@ -795,9 +928,9 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
     bool ok;
     const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
     if (sl >= 0)
-        ok = gcm_record_staged<OPEN, FAST>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
+        ok = gcm_record_staged<OPEN, FAST, CT>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
     else /* a third state in the window: its own context, from global memory */
-        ok = gcm_record_global<OPEN, FAST>(rv, l, TE, tpl);
+        ok = gcm_record_global<OPEN, FAST, CT>(rv, l, TE, tpl);
     if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
 }
 
@@ -810,7 +943,7 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
  * CTR, then GHASH over the CT just written.  Open: GHASH and tag check
  * first, CTR only when the tag verified (cipher-aesgcm.c:184-186).
  */
-template <bool OPEN>
+template <bool OPEN, bool CT>
 __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
 {
     constexpr int K = GCM_LANES;
@@ -828,8 +961,9 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
         te[i] = g_te0[i];
         sb[i] = g_sbox[i];
     }
-    for (uint32_t i = t; i < (uint32_t)GHASH_TAB_ENTRIES; i += 256)
-        h4[i] = ((const uint4 *)ctx->tab[K - 1])[i];
+    if (!CT)
+        for (uint32_t i = t; i < (uint32_t)GHASH_TAB_ENTRIES; i += 256)
+            h4[i] = ((const uint4 *)ctx->tab[K - 1])[i];
     __syncthreads();
     const uint32_t *rk = ctx->rk;
 
@@ -850,9 +984,14 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
         const uint8_t *ct = OPEN ? src : dst;
         const uint32_t A = (d.ad_len + 15) / 16, n = A + M + 1;
         const uint32_t c0 = ((uint32_t)l + n) % K;
+        uint32_t h4n[4] = {0, 0, 0, 0};
+        if constexpr (CT) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) h4n[w] = ctx->hn[K - 1][w];
+        }
         uint32_t acc[4] = {0, 0, 0, 0};
         for (uint32_t i = c0; i < n; i += K) {
-            if (i != c0) gh_mul_lds(acc, h4);
+            if (i != c0) gh_step<CT>(acc, h4, h4n);
             uint32_t x[4];
             if (i < A) {
                 const uint32_t rem = d.ad_len - 16 * i;
@@ -865,13 +1004,15 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
                 x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
                 x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
             }
+            if constexpr (CT) gh_to_nat(x);
             acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
         }
-        gh_mul(acc, (const uint4 *)ctx->tab[K - 1 - l]);
+        gh_scale<CT>(acc, ctx, K - 1 - l);
 #pragma unroll
         for (int off = 1; off < K; off <<= 1)
 #pragma unroll
             for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+        if constexpr (CT) gh_to_nat(acc);
         uint32_t ej[4];
         aes_ctr_block(rk, te, sb, d.nonce, 1u, ej);
         const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};

@@ -64,7 +64,7 @@ class NoiseAeadUniform(C.Structure):
                 ("in_stride", C.c_uint64), ("out_stride", C.c_uint64),
                 ("ad_stride", C.c_uint64), ("recs_per_state", C.c_uint32),
                 ("n_records", C.c_uint32), ("len", C.c_uint32), ("ad_len", C.c_uint32),
-                ("lanes_per_record", C.c_uint32), ("reserved_", C.c_uint32)]
+                ("lanes_per_record", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class NoiseAeadRecord(C.Structure):
@@ -81,6 +81,7 @@ class NoiseAeadRagged(C.Structure):
 
 
 FLAG_FAST = 1
+FLAG_CT_GHASH = 2
 _LIB = None
 
 
@@ -352,10 +353,10 @@ def dev_prepare(cipher: int, d_raw_keys: int, n_states: int, d_ctx: int, stream:
 def dev_uniform(open_: bool, cipher: int, *, ctx: int, nonce_base: int, inp: int, out: int,
                 in_stride: int, out_stride: int, length: int, n_records: int,
                 recs_per_state: int, status: int = 0, ad: int = 0, ad_stride: int = 0,
-                ad_len: int = 0, lanes: int = 0, stream: int = 0) -> int:
+                ad_len: int = 0, lanes: int = 0, flags: int = 0, stream: int = 0) -> int:
     j = NoiseAeadUniform(ctx, nonce_base, inp, out, ad or None, status or None, in_stride,
                          out_stride, ad_stride, recs_per_state, n_records, length, ad_len,
-                         lanes, 0)
+                         lanes, flags)
     f = lib().noise_aead_dev_open_uniform if open_ else lib().noise_aead_dev_seal_uniform
     return f(cipher, C.byref(j), stream or None)
 
@@ -363,10 +364,10 @@ def dev_uniform(open_: bool, cipher: int, *, ctx: int, nonce_base: int, inp: int
 def uniform_job(*, ctx: int, nonce_base: int, inp: int, out: int, in_stride: int,
                 out_stride: int, length: int, n_records: int, recs_per_state: int,
                 status: int = 0, ad: int = 0, ad_stride: int = 0, ad_len: int = 0,
-                lanes: int = 0) -> NoiseAeadUniform:
+                lanes: int = 0, flags: int = 0) -> NoiseAeadUniform:
     return NoiseAeadUniform(ctx, nonce_base, inp, out, ad or None, status or None, in_stride,
                             out_stride, ad_stride, recs_per_state, n_records, length, ad_len,
-                            lanes, 0)
+                            lanes, flags)
 
 
 def dev_duplex(cipher: int, seal_job: NoiseAeadUniform, open_job: NoiseAeadUniform,

@@ -45,7 +45,8 @@ def prepare(aead, cipher, keys):
 
 
 def gpu_uniform(aead, open_, cipher, keys, nonce_base, rps, inp, in_stride, length, count,
-                out_stride, lanes=0, ad=None, ad_stride=0, ad_len=0, out_init=0xA5, out=None):
+                out_stride, lanes=0, ad=None, ad_stride=0, ad_len=0, out_init=0xA5, out=None,
+                flags=0):
     torch = _torch()
     ctx, _k = prepare(aead, cipher, keys)
     d_nb = dev(np.asarray(nonce_base, dtype=np.uint64).view(np.int64))
@@ -61,7 +62,7 @@ def gpu_uniform(aead, open_, cipher, keys, nonce_base, rps, inp, in_stride, leng
                           out_stride=out_stride, length=length, n_records=count,
                           recs_per_state=rps, status=d_st.data_ptr(),
                           ad=d_ad.data_ptr() if d_ad is not None else 0, ad_stride=ad_stride,
-                          ad_len=ad_len, lanes=lanes, stream=stream())
+                          ad_len=ad_len, lanes=lanes, flags=flags, stream=stream())
     assert rc == 0, hex(rc)
     sync()
     return d_out.cpu().numpy(), d_st.cpu().numpy()[:count]
