@@ -435,6 +435,18 @@ NA_DEV void store16(uint8_t *p, uint32_t n, const uint32_t w[4])
     }
 }
 
+/* A rejected record (MAC failure) of an open: in place (dst == src) nothing
+   is written, as in the reference (cipher-chachapoly.c / cipher-aesgcm.c
+   verify before decrypting); out of place its len output bytes become zero,
+   so no unauthenticated plaintext is ever left behind — the single-pass
+   staged open writes plaintext before its verdict.  Lane k of a group of n. */
+NA_DEV void scrub_rejected(uint8_t *dst, const uint8_t *src, uint32_t len, uint32_t k, uint32_t n)
+{
+    if (dst == src) return;
+    const uint32_t z[4] = {0, 0, 0, 0};
+    for (uint32_t o = 16u * k; o < len; o += 16u * n) store16(dst + o, min(16u, len - o), z);
+}
+
 /* 64-byte unit: n valid bytes (1..64), the rest read as zero. */
 NA_DEV void load_unit(const uint8_t *p, uint32_t n, uint32_t w[16])
 {

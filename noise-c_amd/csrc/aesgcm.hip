@@ -463,6 +463,7 @@ __global__ __launch_bounds__(256) void gcm_uniform(UniformArgs a)
     rv.ad_len = a.ad_len;
     const bool ok = gcm_record<OPEN, CT>(rv, l, te, sb);
     if (OPEN && l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, GCM_LANES);
 }
 
 template <bool OPEN, bool CT>
@@ -488,6 +489,7 @@ __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
     rv.ad_len = d.ad_len;
     const bool ok = gcm_record<OPEN, CT>(rv, l, te, sb);
     if (l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, GCM_LANES);
 }
 
 /* ---------------------------- staged (uniform FAST, one state per workgroup)
@@ -749,7 +751,10 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
     load16(src + len, 16, got);
     const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) == 0;
     if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-    if (!ok) return; /* cipher-aesgcm.c:184-186: nothing decrypted */
+    if (!ok) { /* cipher-aesgcm.c:184-186: nothing decrypted */
+        scrub_rejected(dst, src, len, (uint32_t)l, K);
+        return;
+    }
     for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
         const uint4 v = *(const uint4 *)(src + 16 * d);
         uint32_t x[4] = {v.x, v.y, v.z, v.w}, ks[4];
@@ -932,6 +937,7 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
     else /* a third state in the window: its own context, from global memory */
         ok = gcm_record_global<OPEN, FAST, CT>(rv, l, TE, tpl);
     if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, K);
 }
 
 /* ------------------------------------------ wide (small batches, latency)
@@ -1030,7 +1036,10 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
     }
     if (OPEN) {
         __syncthreads();
-        if (!verdict) return; /* nothing decrypted */
+        if (!verdict) { /* nothing decrypted */
+            scrub_rejected(dst, src, len, t, 256);
+            return;
+        }
         for (uint32_t b = t; b < M; b += 256) {
             const uint32_t nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
             uint32_t x[4], ks[4];

@@ -792,6 +792,15 @@ NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
     if (k == K - 1 && live) tag_out(u_dst(a, rc) + len, len, tag);
 }
 
+/* Open, single pass (the structure of seal_il_staged): each step's
+   ciphertext unit goes through Poly1305 and, XORed with its key stream, out
+   as plaintext, so the ciphertext is read once.  The verdict comes after the
+   plaintext is written; a wave holding a rejected record then runs a repair
+   pass (taken only on MAC failure): in place it re-encrypts that record's
+   plaintext back into the ciphertext it was given — the buffer reads as
+   untouched, as after the reference's verify-then-decrypt
+   (cipher-chachapoly.c:140-150) — and out of place it zeroes the record's
+   output (scrub_rejected's contract). */
 template <int K, bool UKEY>
 NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uint32_t blk)
 {
@@ -810,96 +819,89 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
     const int gbase = (int)lane & ~(K - 1);
     const WaveIO<K> io = wave_io<K>(rec0, lane);
     const int last_full = (int)g.J - 2;
-    uint4 *const t0 = tiles, *const t1 = tiles + 256;
+    const uint32_t tail = g.J ? len - 64 * (g.J - 1) : 0; /* bytes of unit J-1 */
 
-    /* step-0 key stream: block 0 (Poly key) on lane o, data on the others;
-       parked in tile 1 until phase 2 */
-    const int v0 = k - (int)g.o;
     Fe acc = fe_zero();
     Mul mr, mjump;
     uint32_t s[4];
-    {
-        uint32_t x0[16];
-        chacha20_block_pre(key, pre, (uint32_t)v0, n_lo, n_hi, x0);
-        tile_put_unit(t1, lane, x0);
-        Fe r;
-        poly_key_bcast(x0, gbase + (int)g.o, r, s);
-        mr = mk_mul(r);
-        Mul mfinal;
-        poly_powers<K>(r, k, g.q, mjump, mfinal);
-        fin_put(fin, lane, mfinal); /* read back after phase 1 */
-    }
-    const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
-    if (k == k0 && a.ad_len) poly_ad(acc, mr, u_ad(a, rc), a.ad_len);
-
-    /* phase 1: authenticate.  No ChaCha to hide behind here (≈220
-       instructions a step), so loads run two steps ahead in registers — one
-       step of lead is shorter than a cold HBM read under load — and tile 0
-       alone re-shapes them. */
     bool seen = false;
-    Quad P1 = wave_load<K>(a, io, -(int)g.o - 1);
-    Quad P2 = wave_load<K>(a, io, g.steps > 1 ? K - (int)g.o - 1 : -(int)g.o - 1);
+    wave_dma<K>(a, io, -(int)g.o - 1, tiles);
     for (uint32_t m = 0; m < g.steps; ++m) {
-        if (a.balance) prio_by_progress(m, 3 * g.steps); /* phase 1: ~1/3 of the work */
+        if (a.balance) prio_by_progress(m, g.steps);
         const int j0 = (int)(m * K) - (int)g.o - 1;
         const int v = j0 + 1 + k;
-        const Quad Pn = wave_load<K>(a, io, m + 2 < g.steps ? j0 + 2 * K : j0);
+        uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
         __builtin_amdgcn_wave_barrier();
-        tile_put_coalesced(t0, lane, P1); /* waits for step m's loads only */
-        P1 = P2;
-        P2 = Pn;
+        if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
+        uint32_t x[16];
+        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        if (m == 0) {
+            Fe r;
+            poly_key_bcast(x, gbase + (int)g.o, r, s);
+            mr = mk_mul(r);
+            Mul mfinal;
+            poly_powers<K>(r, k, g.q, mjump, mfinal);
+            fin_put(fin, lane, mfinal);
+            const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
+            if (k == k0 && a.ad_len) poly_ad(acc, mr, u_ad(a, rc), a.ad_len);
+        }
         __builtin_amdgcn_wave_barrier();
         uint32_t w[16];
-        tile_get_unit(t0, lane, w);
-        if (v >= 1) {
+        tile_get_unit(cur, lane, w);
+        if (v >= 1 && (uint32_t)v <= g.J) {
             uint32_t nb = 4;
-            if ((uint32_t)v == g.J) {
-                const uint32_t bytes = len - 64 * (g.J - 1);
-                mask_unit(w, bytes);
-                nb = (bytes + 15) / 16;
+            if ((uint32_t)v == g.J) { /* bytes past len are never stored */
+                mask_unit(w, tail);
+                nb = (tail + 15) / 16;
             }
             poly_unit(acc, seen ? mjump : mr, mr, w, nb);
             seen = true;
         }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+        if (v >= 1 && (uint32_t)v == g.J && live) last_unit_out(u_dst(a, rc) + 64 * (g.J - 1), tail, w);
+        tile_put_unit(cur, lane, w);
+        __builtin_amdgcn_wave_barrier();
+        wave_store<K>(a, io, j0, last_full, cur, lane, 0xfu);
     }
     uint32_t tag[4], got[4];
     poly_close<K>(acc, k, mr, fin_get(fin, lane), a.ad_len, len, s, tag);
-    tag_in<true>(u_src(a, rc), len, got);
+    tag_in<true>(u_src(a, rc), len, got); /* the tag bytes are never written */
     const bool ok = tag_equal(tag, got);
     if (k == K - 1 && live && a.status) a.status[rec_raw] = ok ? 0 : 1;
-    /* verdict of the owner each coalesced instruction serves */
-    uint32_t okm = 0;
+    const bool bad = live && !ok;
+    if (__ballot(bad) == 0) return; /* wave-uniform: the common case */
+
+    /* repair pass: bit i of badm = the owner coalesced instruction i serves */
+    uint32_t badm = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        okm |= (__shfl((int)ok, (int)(16u * i + (lane >> 2)), 64) != 0 ? 1u : 0u) << i;
-
-    /* phase 2: decrypt, double-buffered by LDS-DMA (the step-0 key stream
-       leaves tile 1 before the first DMA into it) */
-    __builtin_amdgcn_wave_barrier();
-    wave_dma<K>(a, io, -(int)g.o - 1, t0);
+        badm |= (__shfl((int)bad, (int)(16u * i + (lane >> 2)), 64) != 0 ? 1u : 0u) << i;
+    const bool inplace = a.in == a.out && a.in_stride == a.out_stride;
+    __threadfence(); /* this wave's plaintext stores, visible to its reads below */
     for (uint32_t m = 0; m < g.steps; ++m) {
-        if (a.balance) prio_by_progress(g.steps + 2 * m, 3 * g.steps);
         const int j0 = (int)(m * K) - (int)g.o - 1;
         const int v = j0 + 1 + k;
-        uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
-        uint32_t x[16];
-        if (m == 0) {
-            tile_get_unit(t1, lane, x);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
-        if (m != 0) chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
-        __builtin_amdgcn_wave_barrier();
         uint32_t w[16];
-        tile_get_unit(cur, lane, w);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-        if (v >= 1 && (uint32_t)v == g.J && live && ok)
-            last_unit_out(u_dst(a, rc) + 64 * (g.J - 1), len - 64 * (g.J - 1), w);
-        tile_put_unit(cur, lane, w);
         __builtin_amdgcn_wave_barrier();
-        wave_store<K>(a, io, j0, last_full, cur, lane, okm);
+        if (inplace) {
+            wave_dma<K>(a, io, j0, tiles);
+            uint32_t x[16];
+            chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            tile_get_unit(tiles, lane, w);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = 0;
+        }
+        if (v >= 1 && (uint32_t)v == g.J && bad) last_unit_out(u_dst(a, rc) + 64 * (g.J - 1), tail, w);
+        __builtin_amdgcn_wave_barrier();
+        tile_put_unit(tiles, lane, w);
+        __builtin_amdgcn_wave_barrier();
+        wave_store<K>(a, io, j0, last_full, tiles, lane, badm);
     }
 }
 
@@ -1201,8 +1203,10 @@ __global__ __launch_bounds__(256) void chachapoly_open_uniform(UniformArgs a)
     const uint32_t rec = gtid / K;
     if (rec >= a.n_records) return;
     const int k = (int)(gtid % K);
-    const bool ok = open_any<K, FAST>(uniform_view(a, rec), k);
+    const RecView rv = uniform_view(a, rec);
+    const bool ok = open_any<K, FAST>(rv, k);
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)k, K);
 }
 
 /* Ragged batches: the workgroup's 256/K records are taken in length order
@@ -1239,6 +1243,7 @@ __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
         ok = open_any<K, FAST>(rv, k);
     }
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)k, K);
 }
 
 } // namespace na

@@ -3,7 +3,10 @@
 Bit-exact comparisons (integer/byte work): every ciphertext byte and tag must
 equal the CPU oracle's (oracle/noise_oracle.c, itself pinned to the reference
 by tests/test_oracle.py), and every decrypt must reproduce the reference's
-accept/reject decision and leave rejected records untouched.
+accept/reject decision.  A rejected record is left untouched when opened in
+place (the reference verifies before it decrypts) and has its output bytes
+zeroed when opened out of place (scrub_rejected: never unauthenticated
+plaintext).
 """
 import ctypes as C
 import os
@@ -137,7 +140,7 @@ def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed, r
             seg = back[i * in_stride: i * in_stride + L]
             if i in bad:
                 assert st[i] == 1, f"tamper not detected len={L} rec={i}"
-                assert np.all(seg == 0x5A), "rejected record was written"
+                assert np.all(seg == 0), "rejected record's output not zeroed"
             else:
                 assert st[i] == 0, f"valid record rejected len={L} rec={i}"
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L])
@@ -174,10 +177,48 @@ def test_uniform_staged_kernels(aead, gpu, oracle, cipher):
         for i in range(count):
             seg = back[i * in_stride: i * in_stride + L]
             if i in bad:
-                assert st[i] == 1 and np.all(seg == 0x3C), f"len={L} rec={i}"
+                assert st[i] == 1 and np.all(seg == 0), f"len={L} rec={i}"
             else:
                 assert st[i] == 0, f"len={L} rec={i}"
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L]), f"len={L} rec={i}"
+
+
+@pytest.mark.parametrize("cipher,lanes,rps", [(CHACHA, 4, 256), (CHACHA, 4, 13), (CHACHA, 8, 256),
+                                              (CHACHA, 8, 13), (CHACHA, 1, 16), (AES, 0, 256),
+                                              (AES, 0, 13)])
+def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes, rps):
+    """Open in place (in == out, one stride): every verified record becomes
+    its plaintext and every rejected one reads exactly as given — CT and tag
+    bytes — including in the single-pass staged ChaChaPoly kernels, which
+    write plaintext before the verdict and re-encrypt on failure."""
+    torch = _torch()
+    rng = np.random.default_rng(808 + lanes + rps + (cipher & 3))
+    for L, count in [(1400, 700), (0, 70), (17, 300), (4096, 40), (100, 257)]:
+        S = (count + rps - 1) // rps
+        keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
+        nb = rng.integers(0, 2**62, S, dtype=np.uint64)
+        stride_ = (L + 16 + 63) // 64 * 64
+        pt = rng.integers(0, 256, count * stride_ + 64, dtype=np.uint8)
+        ct = oracle_seal_records(oracle, cipher, keys, nb, rps, pt, stride_, L, count, stride_)
+        bad = sorted(set(int(x) for x in rng.integers(0, count, 9)))
+        for b in bad:
+            ct[b * stride_ + int(rng.integers(0, L + 16))] ^= 0x21
+        ctx, _k = prepare(aead, cipher, keys)
+        d_nb = dev(nb.view(np.int64))
+        d_buf = dev(ct)
+        d_st = torch.full((count,), 7, dtype=torch.uint8, device="cuda")
+        assert aead.dev_uniform(True, cipher, ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(),
+                                inp=d_buf.data_ptr(), out=d_buf.data_ptr(), in_stride=stride_,
+                                out_stride=stride_, length=L, n_records=count, recs_per_state=rps,
+                                status=d_st.data_ptr(), lanes=lanes, stream=stream()) == 0
+        sync()
+        back, st = d_buf.cpu().numpy(), d_st.cpu().numpy()
+        for i in range(count):
+            o = i * stride_
+            if i in bad:
+                assert st[i] == 1 and np.array_equal(back[o:o + L + 16], ct[o:o + L + 16]), (L, i)
+            else:
+                assert st[i] == 0 and np.array_equal(back[o:o + L], pt[o:o + L]), (L, i)
 
 
 @pytest.mark.parametrize("cipher,lanes,layout", [(CHACHA, 4, "fast"), (CHACHA, 8, "fast"),
@@ -231,7 +272,7 @@ def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout):
         for i in range(nb_):
             seg = back[i * ib: i * ib + Lb]
             if i in bad:
-                assert st[i] == 1 and np.all(seg == 0x5A), f"duplex open len={Lb} rec={i}"
+                assert st[i] == 1 and np.all(seg == 0), f"duplex open len={Lb} rec={i}"
             else:
                 assert st[i] == 0, f"duplex open len={Lb} rec={i}"
                 assert np.array_equal(seg, ptb[i * ib: i * ib + Lb]), f"len={Lb} rec={i}"
