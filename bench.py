@@ -115,8 +115,8 @@ def mixed_layout(records_per_gpu: int, states: int, rank: int):
                 st_global=st_global, nonce=nonce, rps=rps)
 
 
-def stride(n: int) -> int:
-    return (n + IN_ALIGN - 1) // IN_ALIGN * IN_ALIGN
+def stride(n: int, align: int = IN_ALIGN) -> int:
+    return (n + align - 1) // align * align
 
 
 def physical_cores(cpus):
@@ -303,6 +303,9 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--lanes", type=int, default=0, help="lanes per record (0 = library default)")
     ap.add_argument("--sets", type=int, default=4, help="rotating batch sets (> MALL)")
+    ap.add_argument("--align", type=int, default=IN_ALIGN, choices=(16, 64, 128),
+                    help="record slot alignment of the device batch (strides roundup(len, align), "
+                         "roundup(len + 16, align))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="check every open status after timing")
     ap.add_argument("--no-xfer", action="store_true",
@@ -352,7 +355,7 @@ def main():
             raise SystemExit(f"{args.config}: {N} records / {S} states do not split over {world} ranks")
         N, S = N // world, S // world
     sh = shard(N, S, rank, world)
-    in_stride, out_stride = stride(L), stride(L + 16)
+    in_stride, out_stride = stride(L, args.align), stride(L + 16, args.align)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 

@@ -201,7 +201,6 @@ NA_DEV void gh_to_nat(uint32_t x[4])
 
 /* gh_mul with the table in LDS: lookups taken in pairs so every accumulate is
    one 3-input XOR */
-template <bool THROTTLE = false>
 NA_DEV void gh_mul_lds(uint32_t y[4], const uint4 *tab)
 {
     uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
@@ -213,9 +212,6 @@ NA_DEV void gh_mul_lds(uint32_t y[4], const uint4 *tab)
         const uint4 f = tab[(p + 1) * 16 + (byte & 15)];
         r0 = xor3(r0, e.x, f.x); r1 = xor3(r1, e.y, f.y);
         r2 = xor3(r2, e.z, f.z); r3 = xor3(r3, e.w, f.w);
-        /* THROTTLE: at most 8 table rows (32 VGPRs) in flight, where hipcc
-           would otherwise hoist all 32 reads of an unrolled GHASH-only loop */
-        if (THROTTLE && (p & 6) == 6) asm volatile("" ::: "memory");
     }
     y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
 }
@@ -223,11 +219,11 @@ NA_DEV void gh_mul_lds(uint32_t y[4], const uint4 *tab)
 /* The Horner step y <- y * H^4 (tables in LDS, or constant-time: y and the
    blocks in the natural domain, hn4 = H^4 there) and the final scale
    y <- y * H^(m+1) (the context's tables in global memory, or CT). */
-template <bool CT, bool THROTTLE = false>
+template <bool CT>
 NA_DEV void gh_step(uint32_t y[4], const uint4 *tab_lds, const uint32_t hn4[4])
 {
     if constexpr (CT) gh_mul_ct(y, hn4);
-    else gh_mul_lds<THROTTLE>(y, tab_lds);
+    else gh_mul_lds(y, tab_lds);
 }
 
 template <bool CT>
@@ -694,24 +690,28 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
         for (int w = 0; w < 4; ++w) h4n[w] = ctx->hn[K - 1][w];
     }
     uint32_t acc[4] = {0, 0, 0, 0};
-    AesPre pre;
-    if (!OPEN) pre = aes_pre_lds(TE, L.rk, tpl, n_hi, n_lo);
+    const AesPre pre = aes_pre_lds(TE, L.rk, tpl, n_hi, n_lo);
 #pragma unroll 1
     for (uint32_t i = c0; i < n; i += K) {
-        if (i != c0) gh_step<CT, OPEN>(acc, L.h4, h4n);
+        if (i != c0) gh_step<CT>(acc, L.h4, h4n);
         uint32_t x[4];
         if (i >= A && i < A + M) {
             const uint32_t d = i - A;
             const uint4 v = *(const uint4 *)(src + 16 * d); /* FAST: readable */
             x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
             const uint32_t nb = min(len - 16 * d, 16u);
-            if (!OPEN) {
-                uint32_t ks[4];
-                aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
+            /* CTR for both directions in this one pass: the ciphertext is read
+               once (open: GHASH over the block as read, plaintext out now,
+               repaired below if the tag fails) */
+            uint32_t ks[4], y[4];
+            aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
 #pragma unroll
-                for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
-                if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
-                else store16(dst + 16 * d, nb, x);
+            for (int w = 0; w < 4; ++w) y[w] = x[w] ^ ks[w];
+            if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(y[0], y[1], y[2], y[3]);
+            else store16(dst + 16 * d, nb, y);
+            if (!OPEN) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) x[w] = y[w];
             }
 #pragma unroll
             for (int w = 0; w < 4; ++w) x[w] &= blk_mask(nb, w);
@@ -733,7 +733,6 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
     if constexpr (CT) gh_to_nat(acc);
-    if (OPEN) pre = aes_pre_lds(TE, L.rk, tpl, n_hi, n_lo);
     uint32_t ej[4];
     aes_ctr_pre(TE, L.rk, tpl, pre, 1u, ej);
     const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
@@ -751,12 +750,18 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
     load16(src + len, 16, got);
     const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) == 0;
     if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-    if (!ok) { /* cipher-aesgcm.c:184-186: nothing decrypted */
+    if (ok) return;
+    /* MAC failure (taken only for a forged or damaged record): the reference
+       verifies before decrypting and leaves the buffer untouched
+       (cipher-aesgcm.c:184-186).  In place, XOR the lane's blocks with their
+       key stream once more — the ciphertext as given comes back; out of place,
+       zero the plaintext written (scrub_rejected's contract). */
+    if (dst != src) {
         scrub_rejected(dst, src, len, (uint32_t)l, K);
         return;
     }
     for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
-        const uint4 v = *(const uint4 *)(src + 16 * d);
+        const uint4 v = *(const uint4 *)(dst + 16 * d);
         uint32_t x[4] = {v.x, v.y, v.z, v.w}, ks[4];
         aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
 #pragma unroll
@@ -805,11 +810,10 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
     const uint32_t n = A + M + 1;
     const uint32_t c0 = ((uint32_t)l + n) % K;
     uint32_t acc[4] = {0, 0, 0, 0};
-    AesPre pre;
-    if (!OPEN) pre = aes_pre_lds(TE, rk, tpl, n_hi, n_lo);
+    const AesPre pre = aes_pre_lds(TE, rk, tpl, n_hi, n_lo);
 #pragma unroll 1
     for (uint32_t i = c0; i < n; i += K) {
-        if (i != c0) gh_step<CT, OPEN>(acc, h4, h4n);
+        if (i != c0) gh_step<CT>(acc, h4, h4n);
         uint32_t x[4];
         if (i >= A && i < A + M) {
             const uint32_t d = i - A;
@@ -820,13 +824,17 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
             } else {
                 load16(rv.src + 16 * d, nb, x);
             }
-            if (!OPEN) {
-                uint32_t ks[4];
-                aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
+            /* one pass for both directions (gcm_staged): open decrypts as it
+               authenticates and repairs on a MAC failure */
+            uint32_t ks[4], y[4];
+            aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
 #pragma unroll
-                for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
-                if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
-                else store16(rv.dst + 16 * d, nb, x);
+            for (int w = 0; w < 4; ++w) y[w] = x[w] ^ ks[w];
+            if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(y[0], y[1], y[2], y[3]);
+            else store16(rv.dst + 16 * d, nb, y);
+            if (!OPEN) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) x[w] = y[w];
             }
 #pragma unroll
             for (int w = 0; w < 4; ++w) x[w] &= blk_mask(nb, w);
@@ -847,7 +855,6 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
 #pragma unroll
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
     if constexpr (CT) gh_to_nat(acc);
-    if (OPEN) pre = aes_pre_lds(TE, rk, tpl, n_hi, n_lo);
     uint32_t ej[4];
     aes_ctr_pre(TE, rk, tpl, pre, 1u, ej);
     const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
@@ -858,23 +865,29 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
     uint32_t got[4];
     load16(rv.src + len, 16, got);
     const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) == 0;
-    if (!ok) return false; /* cipher-aesgcm.c:184-186: nothing decrypted */
-    for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
-        const uint32_t nb = min(len - 16 * d, 16u);
-        uint32_t x[4], ks[4];
-        if (FAST) {
-            const uint4 v = *(const uint4 *)(rv.src + 16 * d);
-            x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
-        } else {
-            load16(rv.src + 16 * d, nb, x);
-        }
-        aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
+    if (ok) return true;
+    /* MAC failure: in place, the lane's blocks XORed with their key stream
+       once more give back the ciphertext as given (the reference leaves the
+       buffer untouched, cipher-aesgcm.c:184-186); out of place the caller's
+       scrub_rejected zeroes the plaintext written */
+    if (rv.dst == rv.src) {
+        for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
+            const uint32_t nb = min(len - 16 * d, 16u);
+            uint32_t x[4], ks[4];
+            if (FAST) {
+                const uint4 v = *(const uint4 *)(rv.dst + 16 * d);
+                x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+            } else {
+                load16(rv.dst + 16 * d, nb, x);
+            }
+            aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
-        if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
-        else store16(rv.dst + 16 * d, nb, x);
+            for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+            if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
+            else store16(rv.dst + 16 * d, nb, x);
+        }
     }
-    return true;
+    return false;
 }
 
 /* the cold path: a record whose state has no LDS slot.  Inlined: as an
