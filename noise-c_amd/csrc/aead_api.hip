@@ -198,14 +198,46 @@ bool ct_ghash(uint32_t flags)
     return (flags & NOISE_AEAD_FLAG_CT_GHASH) || env;
 }
 
-template <bool CT>
-KernelFn<RaggedArgs> gcm_ragged_fn(bool open, bool fast, bool big)
+template <bool CT, int WG, int R>
+KernelFn<RaggedArgs> gcm_ragged_pick(bool open, bool fast)
 {
-    if (big)
-        return open ? (fast ? gcm_ragged_staged<true, true, 1024, CT> : gcm_ragged_staged<true, false, 1024, CT>)
-                    : (fast ? gcm_ragged_staged<false, true, 1024, CT> : gcm_ragged_staged<false, false, 1024, CT>);
-    return open ? (fast ? gcm_ragged_staged<true, true, 256, CT> : gcm_ragged_staged<true, false, 256, CT>)
-                : (fast ? gcm_ragged_staged<false, true, 256, CT> : gcm_ragged_staged<false, false, 256, CT>);
+    return open ? (fast ? gcm_ragged_staged<true, true, WG, CT, R> : gcm_ragged_staged<true, false, WG, CT, R>)
+                : (fast ? gcm_ragged_staged<false, true, WG, CT, R> : gcm_ragged_staged<false, false, WG, CT, R>);
+}
+
+/* Ragged AES-GCM launch shape: threads per workgroup and records per group
+   (gcm_ragged_staged).  A workgroup owns its CU (the LDS T-tables), so:
+   R = 2 (pairs of long and short records per group: +21 % records per CU-
+   second on C5's 64 B-16 KiB mix) once the batch still gives every one of
+   the 256 CUs a 512-record window; R = 1 windows of 256 records below that
+   (R = 2 there would idle half the CUs: C5 at N = 1 ran 1.55 vs 0.94 ms,
+   profiles/r02/c5_gcm_shape_ab.jsonl); 256-thread workgroups over 64-record
+   windows for batches too small to give every CU a 1024-thread one.
+   NOISE_AEAD_GCM_SHAPE=w1024r1|w1024r2 forces a shape (A/B runs). */
+struct GcmShape { int wg, r; };
+
+GcmShape gcm_ragged_shape(uint32_t n)
+{
+    static const int forced = [] {
+        const char *e = getenv("NOISE_AEAD_GCM_SHAPE");
+        if (!e) return 0;
+        if (!strcmp(e, "w1024r1")) return 1;
+        if (!strcmp(e, "w1024r2")) return 2;
+        return 0;
+    }();
+    if (forced == 1) return {1024, 1};
+    if (forced == 2) return {1024, 2};
+    if (n >= 256u * 2 * GCM_WG_RECS) return {1024, 2};
+    if (n >= 256u * GCM_WG_RECS) return {1024, 1};
+    return {256, 1};
+}
+
+template <bool CT>
+KernelFn<RaggedArgs> gcm_ragged_fn(bool open, bool fast, GcmShape sh)
+{
+    if (sh.wg == 1024 && sh.r == 2) return gcm_ragged_pick<CT, 1024, 2>(open, fast);
+    if (sh.wg == 1024) return gcm_ragged_pick<CT, 1024, 1>(open, fast);
+    return gcm_ragged_pick<CT, 256, 1>(open, fast);
 }
 
 int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool open)
@@ -334,12 +366,12 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
             return hip_rc(hipGetLastError());
         }
         const bool fast = (job->flags & NOISE_AEAD_FLAG_FAST) != 0;
-        const bool big = job->n_records >= 256u * GCM_WG_RECS;
-        const uint32_t per = big ? GCM_WG_RECS : GCM_WG_RECS / 4;
+        const GcmShape sh = gcm_ragged_shape(job->n_records);
+        const uint32_t per = (uint32_t)(sh.wg / GCM_LANES * sh.r); /* records per window */
         const uint32_t blocks = (job->n_records + per - 1) / per;
-        KernelFn<RaggedArgs> fn = ct ? gcm_ragged_fn<true>(open, fast, big)
-                                     : gcm_ragged_fn<false>(open, fast, big);
-        hipLaunchKernelGGL(fn, dim3(blocks), dim3(big ? 1024 : 256), 0, s, a);
+        KernelFn<RaggedArgs> fn = ct ? gcm_ragged_fn<true>(open, fast, sh)
+                                     : gcm_ragged_fn<false>(open, fast, sh);
+        hipLaunchKernelGGL(fn, dim3(blocks), dim3(sh.wg), 0, s, a);
         return hip_rc(hipGetLastError());
     }
     return NOISE_ERROR_UNKNOWN_ID;

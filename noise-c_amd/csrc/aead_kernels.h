@@ -77,11 +77,12 @@ template <int NREC>
 __device__ __forceinline__ uint32_t window_rec(const RecDesc *recs, uint32_t n, uint32_t base,
                                                uint32_t g, uint32_t *keys)
 {
-    static_assert(NREC >= 2 && NREC <= 256 && (NREC & (NREC - 1)) == 0, "window");
+    static_assert(NREC >= 2 && NREC <= 512 && (NREC & (NREC - 1)) == 0, "window");
+    constexpr uint32_t IB = NREC <= 256 ? 8 : 9; /* index bits below the length */
     const uint32_t t = threadIdx.x, nt = blockDim.x;
     for (uint32_t i = t; i < (uint32_t)NREC; i += nt) {
         const uint32_t rec = base + i;
-        keys[i] = rec < n ? (min(recs[rec].len, 65535u) << 8) | i : 0xFFFFFFFFu; /* 24-bit len key */
+        keys[i] = rec < n ? (min(recs[rec].len, 65535u) << IB) | i : 0xFFFFFFFFu;
     }
     __syncthreads();
     for (uint32_t k = 2; k <= (uint32_t)NREC; k <<= 1)
@@ -99,7 +100,18 @@ __device__ __forceinline__ uint32_t window_rec(const RecDesc *recs, uint32_t n, 
             __syncthreads();
         }
     const uint32_t key = keys[g < (uint32_t)NREC ? g : 0];
-    return (g < (uint32_t)NREC && key != 0xFFFFFFFFu) ? base + (key & 0xFFu) : 0xFFFFFFFFu;
+    return (g < (uint32_t)NREC && key != 0xFFFFFFFFu) ? base + (key & ((1u << IB) - 1u)) : 0xFFFFFFFFu;
+}
+
+/* The rank in the sorted window of the p-th record of group g (of NG groups)
+   when each group runs R records one after another: ranks g, 2NG-1-g, 2NG+g,
+   ... — long records paired with short ones, so every group (and wave) of a
+   workgroup carries about the same number of blocks, while the groups of one
+   wave still see near-equal lengths at each p. */
+template <int NG>
+__device__ __forceinline__ uint32_t snake_rank(uint32_t g, int p)
+{
+    return (p & 1) ? (uint32_t)(p + 1) * NG - 1u - g : (uint32_t)p * NG + g;
 }
 
 /* AES-GCM per-state device context (prepared once per key). */

@@ -903,11 +903,16 @@ __device__ __forceinline__ bool gcm_record_global(const GcmView &rv, int l,
 }
 
 /* WG threads per workgroup (1024, or 256 for batches too small to give
-   every CU a 1024-thread workgroup); WG / 4 records per window */
-template <bool OPEN, bool FAST, int WG, bool CT>
+   every CU a 1024-thread workgroup); WG / 4 record groups, each running R
+   records of the window's R * WG / 4 one after another (snake_rank).  The
+   T-tables hold the CU's LDS, so a workgroup owns its CU until its longest
+   wave ends: with R = 1 a window of mixed lengths leaves most waves idle
+   while the one holding the longest records finishes; R = 2 pairs long with
+   short records so every wave carries about the window's mean. */
+template <bool OPEN, bool FAST, int WG, bool CT, int R = 1>
 __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
 {
-    constexpr int K = GCM_LANES, NREC = WG / GCM_LANES;
+    constexpr int K = GCM_LANES, NG = WG / GCM_LANES, NREC = NG * R;
     __shared__ GcmLdsR<NREC> L;
     const uint8_t *TE = (const uint8_t *)&L.te[0][0][0];
     const uint32_t base = blockIdx.x * (uint32_t)NREC;
@@ -928,29 +933,42 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
             for (int i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += WG) L.h4[sl][i] = src[i];
         if (threadIdx.x < 60) L.rk[sl][threadIdx.x] = ctx->rk[threadIdx.x];
     }
-    const uint32_t rec = window_rec<NREC>(a.recs, a.n_records, base, threadIdx.x / K, L.order);
-    if (rec >= a.n_records) return;
+    const uint32_t g = threadIdx.x / K;
+    if constexpr (R > 1) { /* sort the whole window; groups take ranks by snake_rank */
+        window_rec<NREC>(a.recs, a.n_records, base, 0, L.order);
+    }
     const int l = (int)(threadIdx.x % K);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t tpl = (1u << 16) | ((128u + 4u * (lane & 31)) << 8) | (4u * (lane & 31));
-    const RecDesc d = a.recs[rec];
-    if (reject_len(a, rec, d.len, l == K - 1)) return;
-    GcmView rv;
-    rv.src = a.in + d.in_off;
-    rv.dst = a.out + d.out_off;
-    rv.ad = a.ad ? a.ad + d.ad_off : nullptr;
-    rv.ctx = (const AesCtx *)(a.keys + d.ctx_off);
-    rv.nonce = d.nonce;
-    rv.len = d.len;
-    rv.ad_len = d.ad_len;
-    bool ok;
-    const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
-    if (sl >= 0)
-        ok = gcm_record_staged<OPEN, FAST, CT>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
-    else /* a third state in the window: its own context, from global memory */
-        ok = gcm_record_global<OPEN, FAST, CT>(rv, l, TE, tpl);
-    if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, K);
+#pragma unroll 1
+    for (int p = 0; p < R; ++p) {
+        uint32_t rec;
+        if constexpr (R == 1) {
+            rec = window_rec<NREC>(a.recs, a.n_records, base, g, L.order);
+        } else {
+            const uint32_t key = L.order[snake_rank<NG>(g, p)];
+            rec = key != 0xFFFFFFFFu ? base + (key & (NREC <= 256 ? 0xFFu : 0x1FFu)) : 0xFFFFFFFFu;
+        }
+        if (rec >= a.n_records) continue;
+        const RecDesc d = a.recs[rec];
+        if (reject_len(a, rec, d.len, l == K - 1)) continue;
+        GcmView rv;
+        rv.src = a.in + d.in_off;
+        rv.dst = a.out + d.out_off;
+        rv.ad = a.ad ? a.ad + d.ad_off : nullptr;
+        rv.ctx = (const AesCtx *)(a.keys + d.ctx_off);
+        rv.nonce = d.nonce;
+        rv.len = d.len;
+        rv.ad_len = d.ad_len;
+        bool ok;
+        const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
+        if (sl >= 0)
+            ok = gcm_record_staged<OPEN, FAST, CT>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
+        else /* a third state in the window: its own context, from global memory */
+            ok = gcm_record_global<OPEN, FAST, CT>(rv, l, TE, tpl);
+        if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+        if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, K);
+    }
 }
 
 /* ------------------------------------------ wide (small batches, latency)

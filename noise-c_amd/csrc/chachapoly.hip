@@ -366,6 +366,91 @@ NA_DEV void seal_il(const RecView &rv, int k)
     if (k == K - 1) tail_out<FAST, true>(rv.dst, g.J, len, w, tag);
 }
 
+/* Open in one pass (FAST layouts): seal_il's loop with Poly1305 over the
+   ciphertext as read, each unit decrypted and stored as it goes, so the
+   ciphertext is read once.  The verdict comes after the plaintext is written:
+   on a MAC failure in place the lane XORs its units with their key stream
+   once more — the buffer reads as given, as after the reference's verify-
+   then-decrypt (cipher-chachapoly.c:125-143) — and out of place the caller's
+   scrub_rejected zeroes the output. */
+template <int K>
+NA_DEV bool open_il_1p(const RecView &rv, int k)
+{
+    uint32_t key[8];
+    load_key(rv.key, key);
+    const uint32_t n_lo = (uint32_t)rv.nonce, n_hi = (uint32_t)(rv.nonce >> 32);
+    ChaPre pre;
+    chacha_pre(key, n_lo, n_hi, pre);
+    const uint32_t len = rv.len;
+    const GroupCtx<K> g = group_ctx<K>(len);
+    const int gbase = (int)(threadIdx.x & 63) & ~(K - 1);
+    const uint32_t tail = g.J ? len - 64 * (g.J - 1) : 0; /* bytes of unit J-1 */
+
+    Fe acc = fe_zero(), r;
+    Mul mr, mjump, mfinal;
+    uint32_t s[4], wn[16], wc[16], x[16];
+    bool seen = false;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wn[i] = 0;
+    {
+        const int v = k - (int)g.o;
+        unit_prefetch<true>(rv.src, v >= 1, (uint32_t)v - 1, len, wn);
+    }
+    for (uint32_t m = 0; m < g.steps; ++m) {
+        const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wc[i] = wn[i];
+        const int vn = v + K;
+        unit_prefetch<true>(rv.src, m + 1 < g.steps && vn >= 1, (uint32_t)vn - 1, len, wn);
+        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        if (m == 0) {
+            poly_key_bcast(x, gbase + (int)g.o, r, s);
+            mr = mk_mul(r);
+            poly_powers<K>(r, k, g.q, mjump, mfinal);
+            const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
+            if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
+        }
+        if (v >= 1 && (uint32_t)v < g.J) { /* a full unit */
+            poly_unit(acc, seen ? mjump : mr, mr, wc, 4);
+            seen = true;
+            uint32_t w[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = wc[i] ^ x[i];
+            unit_out_full<true>(rv.dst + 64 * (v - 1), w);
+        }
+    }
+    /* the last unit (block J) is lane K-1's last step */
+    if (k == K - 1 && g.J >= 1) {
+        uint32_t c[16], w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            c[i] = wc[i];
+            w[i] = wc[i] ^ x[i];
+        }
+        mask_unit(c, tail);
+        poly_unit(acc, seen ? mjump : mr, mr, c, (tail + 15) / 16);
+        tail_out<true, false>(rv.dst, g.J, len, w, nullptr);
+    }
+    uint32_t tag[4], got[4];
+    poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
+    tag_in<true>(rv.src, len, got); /* the tag bytes are never written */
+    const bool ok = tag_equal(tag, got);
+    if (ok || rv.dst != rv.src) return ok;
+    /* repair in place: plaintext XOR key stream = the ciphertext as given */
+    for (uint32_t m = 0; m < g.steps; ++m) {
+        const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
+        if (v < 1) continue;
+        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        uint32_t w[16];
+        unit_in<true>(rv.dst, (uint32_t)v - 1, len, w);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+        if ((uint32_t)v < g.J) unit_out_full<true>(rv.dst + 64 * (v - 1), w);
+        else tail_out<true, false>(rv.dst, g.J, len, w, nullptr);
+    }
+    return false;
+}
+
 /* Open's authentication pass has only Poly1305 (≈200 instructions per unit)
    to hide each unit's load behind, so with one unit prefetched in registers
    it waits on memory.  The FAST ragged kernels stream it through a ring of
@@ -1235,11 +1320,18 @@ __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
     const RecView rv = ragged_view(a, rec);
     if (reject_len(a, rec, rv.len, k == K - 1)) return;
     bool ok;
+#ifdef NA_RAGGED_OPEN_RING
     if constexpr (FAST && K >= 4) {
         __shared__ uint4 r0[4][256], r1[4][256], r2[4][256]; /* 3 x 4 KB per wave */
         const uint32_t w = threadIdx.x >> 6;
         ok = open_il<K, true, true>(rv, k, AuthRing{r0[w], r1[w], r2[w]});
-    } else {
+    } else
+#else
+    if constexpr (FAST && K >= 4) {
+        ok = open_il_1p<K>(rv, k); /* one pass: the ciphertext is read once */
+    } else
+#endif
+    {
         ok = open_any<K, FAST>(rv, k);
     }
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;

@@ -497,6 +497,70 @@ def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, lanes, fast
             assert np.array_equal(back[o:o + L], pt[o:o + L]), i
 
 
+def test_ragged_aes_paired_windows(aead, gpu, oracle):
+    """A ragged AES-GCM batch large enough for the paired shape (>= 131072
+    records: 512-record windows, each 4-lane group running a long and a short
+    record one after the other, gcm_ragged_staged<.., R = 2>), with per-state
+    runs of 300 records (windows holding 2 and 3 states), out of place:
+    a sample of records against the oracle, every record's round trip, and
+    tampered records rejected with their output zeroed."""
+    torch = _torch()
+    rng = np.random.default_rng(4711)
+    count, run = 140_000, 300
+    S = (count + run - 1) // run
+    keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
+    ctx, _k = prepare(aead, AES, keys)
+    cb = aead.dev_ctx_bytes(AES)
+    lens = rng.integers(0, 1200, count)
+    lens[::211] = 9000
+    slot = (lens + 16 + 63) // 64 * 64
+    offs = np.zeros(count, dtype=np.int64)
+    offs[1:] = np.cumsum(slot)[:-1]
+    total = int(offs[-1] + slot[-1]) + 64
+    pt = rng.integers(0, 256, total, dtype=np.uint8)
+    nonces = rng.integers(0, 2**62, count, dtype=np.int64).astype(np.uint64)
+    dt = [("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "<u8"),
+          ("ad_off", "<u8"), ("len", "<u4"), ("ad_len", "<u4")]
+    recs = np.zeros(count, dtype=dt)
+    recs["in_off"] = recs["out_off"] = offs
+    recs["nonce"] = nonces
+    recs["ctx_off"] = (np.arange(count) // run).astype(np.uint64) * cb
+    recs["len"] = lens
+    d_recs = dev(recs.view(np.uint8))
+    d_pt = dev(pt)
+    d_ct = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    assert aead.dev_ragged(False, AES, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
+                           inp=d_pt.data_ptr(), out=d_ct.data_ptr(), n_records=count,
+                           flags=aead.FLAG_FAST, stream=stream()) == 0
+    sync()
+    ct = d_ct.cpu().numpy()
+    for i in list(rng.choice(count, 400, replace=False)) + list(range(0, count, 211)[:40]) + [count - 1]:
+        o, L = int(offs[i]), int(lens[i])
+        exp = oracle.encrypt(AES, bytes(keys[i // run]), int(nonces[i]), bytes(pt[o:o + L]))
+        assert bytes(ct[o:o + L + 16]) == exp, i
+    bad = np.arange(count) % 997 == 13
+    for i in np.nonzero(bad)[0]:
+        ct[int(offs[i]) + int(rng.integers(0, int(lens[i]) + 16))] ^= 0x08
+    d_ct = dev(ct)
+    d_back = torch.full((total,), 0x5A, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((count,), 9, dtype=torch.uint8, device="cuda")
+    assert aead.dev_ragged(True, AES, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
+                           inp=d_ct.data_ptr(), out=d_back.data_ptr(), n_records=count,
+                           status=d_st.data_ptr(), flags=aead.FLAG_FAST, stream=stream()) == 0
+    sync()
+    st, back = d_st.cpu().numpy(), d_back.cpu().numpy()
+    assert np.array_equal(st != 0, bad) and set(np.unique(st)) <= {0, 1}
+    keep = np.zeros(total, dtype=bool)
+    for i in range(count):
+        keep[int(offs[i]):int(offs[i]) + int(lens[i])] = True
+    good_bytes = keep.copy()
+    for i in np.nonzero(bad)[0]:
+        o, L = int(offs[i]), int(lens[i])
+        assert not back[o:o + L].any(), i
+        good_bytes[o:o + L] = False
+    assert np.array_equal(back[good_bytes], pt[good_bytes])
+
+
 # ------------------------------------------- the CipherState API on the GPU
 
 def test_golden_grid_through_cipherstate(aead, gpu, oracle, golden):
