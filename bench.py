@@ -303,7 +303,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--lanes", type=int, default=0, help="lanes per record (0 = library default)")
     ap.add_argument("--sets", type=int, default=4, help="rotating batch sets (> MALL)")
-    ap.add_argument("--align", type=int, default=IN_ALIGN, choices=(16, 64, 128),
+    ap.add_argument("--align", type=int, default=IN_ALIGN, choices=(16, 64, 128, 256),
                     help="record slot alignment of the device batch (strides roundup(len, align), "
                          "roundup(len + 16, align))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
