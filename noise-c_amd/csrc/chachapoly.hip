@@ -712,6 +712,20 @@ NA_DEV void wave_dma(const UniformArgs &a, const WaveIO<K> &io, int j0, uint4 *t
             (lds_void *)(t + 64 * i), 16, 0, 0);
 }
 
+/* A 16-B record store of the staged kernels.  NA_NT_STORE: non-temporal
+   (streaming) — the written lines need not displace the ciphertext lines
+   the next step of an open still reads from L2. */
+typedef uint32_t na_u32x4 __attribute__((ext_vector_type(4)));
+NA_DEV void rec_store16(uint8_t *p, const uint4 &q)
+{
+#ifdef NA_NT_STORE
+    na_u32x4 v = {q.x, q.y, q.z, q.w};
+    __builtin_nontemporal_store(v, (na_u32x4 *)p);
+#else
+    *(uint4 *)p = q;
+#endif
+}
+
 /* Coalesced stores of the step's full units (unit <= last_full) from the
    tile; okm bit i gates instruction i (open: the owner's verdict). */
 template <int K>
@@ -726,7 +740,7 @@ NA_DEV void wave_store(const UniformArgs &a, const WaveIO<K> &io, int j0, int la
         const uint4 q = t[tile_slot(16u * i + (lane >> 2), lane & 3)];
         const uint32_t r = wave_rec(io, i);
         if (r < a.n_records && ((okm >> i) & 1))
-            *(uint4 *)(a.out + (size_t)r * a.out_stride + off) = q;
+            rec_store16(a.out + (size_t)r * a.out_stride + off, q);
     }
 }
 
