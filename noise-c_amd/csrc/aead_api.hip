@@ -198,23 +198,27 @@ bool ct_ghash(uint32_t flags)
     return (flags & NOISE_AEAD_FLAG_CT_GHASH) || env;
 }
 
-template <bool CT, int WG, int R>
+template <bool CT, int WG, int R, int KL = GCM_LANES>
 KernelFn<RaggedArgs> gcm_ragged_pick(bool open, bool fast)
 {
-    return open ? (fast ? gcm_ragged_staged<true, true, WG, CT, R> : gcm_ragged_staged<true, false, WG, CT, R>)
-                : (fast ? gcm_ragged_staged<false, true, WG, CT, R> : gcm_ragged_staged<false, false, WG, CT, R>);
+    return open ? (fast ? gcm_ragged_staged<true, true, WG, CT, R, KL>
+                        : gcm_ragged_staged<true, false, WG, CT, R, KL>)
+                : (fast ? gcm_ragged_staged<false, true, WG, CT, R, KL>
+                        : gcm_ragged_staged<false, false, WG, CT, R, KL>);
 }
 
-/* Ragged AES-GCM launch shape: threads per workgroup and records per group
-   (gcm_ragged_staged).  A workgroup owns its CU (the LDS T-tables), so:
-   R = 2 (pairs of long and short records per group: +21 % records per CU-
-   second on C5's 64 B-16 KiB mix) once the batch still gives every one of
-   the 256 CUs a 512-record window; R = 1 windows of 256 records below that
-   (R = 2 there would idle half the CUs: C5 at N = 1 ran 1.55 vs 0.94 ms,
-   profiles/r02/c5_gcm_shape_ab.jsonl); 256-thread workgroups over 64-record
-   windows for batches too small to give every CU a 1024-thread one.
-   NOISE_AEAD_GCM_SHAPE=w1024r1|w1024r2 forces a shape (A/B runs). */
-struct GcmShape { int wg, r; };
+/* Ragged AES-GCM launch shape: threads per workgroup, records per group
+   and lanes per record (gcm_ragged_staged).  A workgroup owns its CU (the
+   LDS T-tables), so its time is its longest wave's; pairing a long with a
+   short record per group (R = 2) evens the waves out: +21 % records per
+   CU-second on C5's 64 B-16 KiB mix (profiles/r02/c5_gcm_shape_ab.jsonl).
+   From 131072 records on every CU gets a 512-record window of 4-lane groups;
+   from 65536 on, 256-record windows of 8-lane groups (KL = 8, H^8 Horner)
+   keep all CUs busy with the same pairing (4-lane pairs there would idle
+   half the CUs: 1.55 vs 0.94 ms); smaller batches take 256-thread
+   workgroups over 64-record windows.  NOISE_AEAD_GCM_SHAPE=w1024r1 |
+   w1024r2 | w1024r2k8 forces a shape (A/B runs). */
+struct GcmShape { int wg, r, kl; };
 
 GcmShape gcm_ragged_shape(uint32_t n)
 {
@@ -223,18 +227,21 @@ GcmShape gcm_ragged_shape(uint32_t n)
         if (!e) return 0;
         if (!strcmp(e, "w1024r1")) return 1;
         if (!strcmp(e, "w1024r2")) return 2;
+        if (!strcmp(e, "w1024r2k8")) return 3;
         return 0;
     }();
-    if (forced == 1) return {1024, 1};
-    if (forced == 2) return {1024, 2};
-    if (n >= 256u * 2 * GCM_WG_RECS) return {1024, 2};
-    if (n >= 256u * GCM_WG_RECS) return {1024, 1};
-    return {256, 1};
+    if (forced == 1) return {1024, 1, 4};
+    if (forced == 2) return {1024, 2, 4};
+    if (forced == 3) return {1024, 2, 8};
+    if (n >= 256u * 2 * GCM_WG_RECS) return {1024, 2, 4};
+    if (n >= 256u * GCM_WG_RECS) return {1024, 2, 8};
+    return {256, 1, 4};
 }
 
 template <bool CT>
 KernelFn<RaggedArgs> gcm_ragged_fn(bool open, bool fast, GcmShape sh)
 {
+    if (sh.kl == 8) return gcm_ragged_pick<CT, 1024, 2, 8>(open, fast);
     if (sh.wg == 1024 && sh.r == 2) return gcm_ragged_pick<CT, 1024, 2>(open, fast);
     if (sh.wg == 1024) return gcm_ragged_pick<CT, 1024, 1>(open, fast);
     return gcm_ragged_pick<CT, 256, 1>(open, fast);
@@ -367,7 +374,7 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
         }
         const bool fast = (job->flags & NOISE_AEAD_FLAG_FAST) != 0;
         const GcmShape sh = gcm_ragged_shape(job->n_records);
-        const uint32_t per = (uint32_t)(sh.wg / GCM_LANES * sh.r); /* records per window */
+        const uint32_t per = (uint32_t)(sh.wg / sh.kl * sh.r); /* records per window */
         const uint32_t blocks = (job->n_records + per - 1) / per;
         KernelFn<RaggedArgs> fn = ct ? gcm_ragged_fn<true>(open, fast, sh)
                                      : gcm_ragged_fn<false>(open, fast, sh);

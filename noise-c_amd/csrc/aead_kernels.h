@@ -125,6 +125,10 @@ struct AesCtx {
     uint32_t tab[GCM_LANES][GHASH_TAB_ENTRIES][4];
     /* hn[m]: H^(m+1) in the natural polynomial domain (constant-time GHASH) */
     uint32_t hn[GCM_LANES][4];
+    /* H^8: the Horner step of 8-lane record groups (gcm_ragged_staged KL = 8),
+       as a multiply table and in the natural domain */
+    uint32_t tab8[GHASH_TAB_ENTRIES][4];
+    uint32_t hn8[4];
 };
 
 } // namespace na

@@ -227,7 +227,7 @@ NA_DEV void gh_step(uint32_t y[4], const uint4 *tab_lds, const uint32_t hn4[4])
 }
 
 template <bool CT>
-NA_DEV void gh_scale(uint32_t y[4], const AesCtx *ctx, int m)
+NA_DEV void gh_scale1(uint32_t y[4], const AesCtx *ctx, int m)
 {
     if constexpr (CT) {
         uint32_t h[4];
@@ -237,6 +237,18 @@ NA_DEV void gh_scale(uint32_t y[4], const AesCtx *ctx, int m)
     } else {
         gh_mul(y, (const uint4 *)ctx->tab[m]);
     }
+}
+
+/* y <- y * H^(m+1), m < K (lanes per record): K = 8 lanes 0..3 take
+   H^(m+1) = H^4 * H^(m-3) */
+template <bool CT, int K = GCM_LANES>
+NA_DEV void gh_scale(uint32_t y[4], const AesCtx *ctx, int m)
+{
+    if (K > GCM_LANES && m >= GCM_LANES) {
+        gh_scale1<CT>(y, ctx, GCM_LANES - 1);
+        m -= GCM_LANES;
+    }
+    gh_scale1<CT>(y, ctx, m);
 }
 
 /* ----------------------------------------------------------- key prepare */
@@ -267,8 +279,8 @@ __global__ __launch_bounds__(256) void gcm_prepare(const uint8_t *__restrict__ r
                                                    AesCtx *__restrict__ ctx, uint32_t n_states)
 {
     __shared__ uint32_t te[256], sb[256], rk[60];
-    __shared__ uint8_t hp[GCM_LANES][16];       /* H^1..H^4, bytes */
-    __shared__ uint8_t V[GCM_LANES][128][16];   /* x^i * H^m */
+    __shared__ uint8_t hp[GCM_LANES + 1][16];       /* H^1..H^4, H^8, bytes */
+    __shared__ uint8_t V[GCM_LANES + 1][128][16];   /* x^i * H^m */
     const uint32_t st = blockIdx.x;
     if (st >= n_states) return;
     const int t = threadIdx.x;
@@ -300,9 +312,10 @@ __global__ __launch_bounds__(256) void gcm_prepare(const uint8_t *__restrict__ r
         const uint32_t hw[4] = {s0, s1, s2, s3};
         for (int i = 0; i < 16; ++i) hp[0][i] = (uint8_t)(hw[i >> 2] >> (24 - 8 * (i & 3)));
         for (int m = 1; m < GCM_LANES; ++m) gf_mul_bytes(hp[m - 1], hp[0], hp[m]);
+        gf_mul_bytes(hp[GCM_LANES - 1], hp[GCM_LANES - 1], hp[GCM_LANES]); /* H^8 */
     }
     __syncthreads();
-    if (t < GCM_LANES) {
+    if (t < GCM_LANES + 1) {
         uint8_t v[16];
         for (int j = 0; j < 16; ++j) v[j] = hp[t][j];
         for (int i = 0; i < 128; ++i) {
@@ -318,22 +331,23 @@ __global__ __launch_bounds__(256) void gcm_prepare(const uint8_t *__restrict__ r
         for (int j = 0; j < 4; ++j) w |= (uint32_t)hp[0][4 * t + j] << (8 * j);
         c->h[t] = w;
     }
-    if (t < 4 * GCM_LANES) { /* H^1..H^4, natural domain */
+    if (t < 4 * (GCM_LANES + 1)) { /* H^1..H^4, H^8, natural domain */
         const int m = t >> 2, q = t & 3;
         uint32_t w = 0;
         for (int j = 0; j < 4; ++j) w |= (uint32_t)hp[m][4 * q + j] << (8 * j);
-        c->hn[m][q] = gh_nat(w);
+        if (m < GCM_LANES) c->hn[m][q] = gh_nat(w);
+        else c->hn8[q] = gh_nat(w);
     }
-    for (int e = t; e < GCM_LANES * GHASH_TAB_ENTRIES; e += 256) {
+    for (int e = t; e < (GCM_LANES + 1) * GHASH_TAB_ENTRIES; e += 256) {
         const int m = e / GHASH_TAB_ENTRIES, p = (e / 16) % 32, val = e % 16;
         uint8_t acc[16] = {0};
         for (int bit = 0; bit < 4; ++bit)
             if ((val >> (3 - bit)) & 1)
                 for (int j = 0; j < 16; ++j) acc[j] ^= V[m][4 * p + bit][j];
+        uint32_t *dst = m < GCM_LANES ? c->tab[m][p * 16 + val] : c->tab8[p * 16 + val];
         for (int w = 0; w < 4; ++w)
-            c->tab[m][p * 16 + val][w] = (uint32_t)acc[4 * w] | ((uint32_t)acc[4 * w + 1] << 8) |
-                                         ((uint32_t)acc[4 * w + 2] << 16) |
-                                         ((uint32_t)acc[4 * w + 3] << 24);
+            dst[w] = (uint32_t)acc[4 * w] | ((uint32_t)acc[4 * w + 1] << 8) |
+                     ((uint32_t)acc[4 * w + 2] << 16) | ((uint32_t)acc[4 * w + 3] << 24);
     }
 }
 
@@ -794,15 +808,18 @@ struct GcmLdsR {
 /* One record, 4 lanes (l = 0..3): gcm_staged's GHASH/CTR core with the
    record's tables passed in; FAST as in chachapoly.hip (16-B aligned record,
    input readable to roundup16). */
-template <bool OPEN, bool FAST, bool CT>
+template <bool OPEN, bool FAST, bool CT, int KL = GCM_LANES>
 NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint32_t tpl,
                               const uint32_t *rk, const uint4 *h4)
 {
-    constexpr int K = GCM_LANES;
+    /* KL lanes per record (4, or 8 with the H^8 Horner table): the Horner
+       step is H^KL, h4 its multiply table */
+    constexpr int K = KL;
+    static_assert(K == 4 || K == 8, "lanes per AES-GCM record");
     uint32_t h4n[4] = {0, 0, 0, 0};
     if constexpr (CT) {
 #pragma unroll
-        for (int w = 0; w < 4; ++w) h4n[w] = rv.ctx->hn[K - 1][w];
+        for (int w = 0; w < 4; ++w) h4n[w] = K == 8 ? rv.ctx->hn8[w] : rv.ctx->hn[K - 1][w];
     }
     const uint32_t n_hi = (uint32_t)(rv.nonce >> 32), n_lo = (uint32_t)rv.nonce;
     const uint32_t len = rv.len, ad_len = rv.ad_len;
@@ -849,7 +866,7 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
         if constexpr (CT) gh_to_nat(x);
         acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
     }
-    gh_scale<CT>(acc, rv.ctx, K - 1 - l);
+    gh_scale<CT, K>(acc, rv.ctx, K - 1 - l);
 #pragma unroll
     for (int off = 1; off < K; off <<= 1)
 #pragma unroll
@@ -894,25 +911,32 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
    out-of-line call its frame and caller-saved registers cost the slot path
    scratch traffic (open 176 -> 104 B/lane, seal 64 -> 0) and C5's AES
    kernels 2-5 % (profiles/r01_aes_inline_ab.jsonl). */
-template <bool OPEN, bool FAST, bool CT>
+template <int KL>
+NA_DEV const uint4 *horner_tab(const AesCtx *ctx)
+{
+    return (const uint4 *)(KL == 8 ? ctx->tab8 : ctx->tab[GCM_LANES - 1]);
+}
+
+template <bool OPEN, bool FAST, bool CT, int KL>
 __device__ __forceinline__ bool gcm_record_global(const GcmView &rv, int l,
                                                   const uint8_t *TE, uint32_t tpl)
 {
-    return gcm_record_staged<OPEN, FAST, CT>(rv, l, TE, tpl, rv.ctx->rk,
-                                             (const uint4 *)rv.ctx->tab[GCM_LANES - 1]);
+    return gcm_record_staged<OPEN, FAST, CT, KL>(rv, l, TE, tpl, rv.ctx->rk, horner_tab<KL>(rv.ctx));
 }
 
 /* WG threads per workgroup (1024, or 256 for batches too small to give
-   every CU a 1024-thread workgroup); WG / 4 record groups, each running R
-   records of the window's R * WG / 4 one after another (snake_rank).  The
-   T-tables hold the CU's LDS, so a workgroup owns its CU until its longest
-   wave ends: with R = 1 a window of mixed lengths leaves most waves idle
-   while the one holding the longest records finishes; R = 2 pairs long with
-   short records so every wave carries about the window's mean. */
-template <bool OPEN, bool FAST, int WG, bool CT, int R = 1>
+   every CU a 1024-thread workgroup); WG / KL record groups of KL lanes (4,
+   or 8 with the H^8 Horner table), each running R records of the window's
+   R * WG / KL one after another (snake_rank).  The T-tables hold the CU's
+   LDS, so a workgroup owns its CU until its longest wave ends: with R = 1 a
+   window of mixed lengths leaves most waves idle while the one holding the
+   longest records finishes; R = 2 pairs long with short records so every
+   wave carries about the window's mean (KL = 8 keeps that at 256 records
+   per window). */
+template <bool OPEN, bool FAST, int WG, bool CT, int R = 1, int KL = GCM_LANES>
 __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
 {
-    constexpr int K = GCM_LANES, NG = WG / GCM_LANES, NREC = NG * R;
+    constexpr int K = KL, NG = WG / KL, NREC = NG * R;
     __shared__ GcmLdsR<NREC> L;
     const uint8_t *TE = (const uint8_t *)&L.te[0][0][0];
     const uint32_t base = blockIdx.x * (uint32_t)NREC;
@@ -928,7 +952,7 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
         const AesCtx *ctx = (const AesCtx *)(a.keys + slot_off[sl]);
-        const uint4 *src = (const uint4 *)ctx->tab[K - 1];
+        const uint4 *src = horner_tab<KL>(ctx);
         if (!CT)
             for (int i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += WG) L.h4[sl][i] = src[i];
         if (threadIdx.x < 60) L.rk[sl][threadIdx.x] = ctx->rk[threadIdx.x];
@@ -963,9 +987,9 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
         bool ok;
         const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
         if (sl >= 0)
-            ok = gcm_record_staged<OPEN, FAST, CT>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
+            ok = gcm_record_staged<OPEN, FAST, CT, KL>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
         else /* a third state in the window: its own context, from global memory */
-            ok = gcm_record_global<OPEN, FAST, CT>(rv, l, TE, tpl);
+            ok = gcm_record_global<OPEN, FAST, CT, KL>(rv, l, TE, tpl);
         if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
         if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, K);
     }

@@ -497,16 +497,19 @@ def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, lanes, fast
             assert np.array_equal(back[o:o + L], pt[o:o + L]), i
 
 
-def test_ragged_aes_paired_windows(aead, gpu, oracle):
-    """A ragged AES-GCM batch large enough for the paired shape (>= 131072
-    records: 512-record windows, each 4-lane group running a long and a short
-    record one after the other, gcm_ragged_staged<.., R = 2>), with per-state
-    runs of 300 records (windows holding 2 and 3 states), out of place:
-    a sample of records against the oracle, every record's round trip, and
-    tampered records rejected with their output zeroed."""
+@pytest.mark.parametrize("count", [70_000, 140_000])
+def test_ragged_aes_paired_windows(aead, gpu, oracle, count):
+    """Ragged AES-GCM batches large enough for the paired shapes, where each
+    record group runs a long and a short record one after the other
+    (gcm_ragged_staged<.., R = 2>): 70 000 records take 256-record windows of
+    8-lane groups (the H^8 Horner table), 140 000 take 512-record windows of
+    4-lane groups.  Per-state runs of 300 records (windows holding 2 and 3
+    states), out of place: a sample of records against the oracle, every
+    record's round trip, and tampered records rejected with their output
+    zeroed."""
     torch = _torch()
-    rng = np.random.default_rng(4711)
-    count, run = 140_000, 300
+    rng = np.random.default_rng(4711 + count)
+    run = 300
     S = (count + run - 1) // run
     keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
     ctx, _k = prepare(aead, AES, keys)
