@@ -785,8 +785,10 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     # the kernel the library dispatches (aead_api.hip run_ragged), as rocprofv3 names it
     if g["cipher"] == CHACHA:
         kname = f"chachapoly_{'open' if open_ else 'seal'}_ragged<{args.lanes or 4}, true>"
-    else:
-        kname = f"gcm_ragged_staged<{'true' if open_ else 'false'}, true, 1024, false>"
+    else:  # gcm_ragged_shape: (threads, records per group, lanes per record) by batch size
+        n_aes = g["n"]
+        wg, r, kl = (1024, 2, 4) if n_aes >= 131072 else ((1024, 2, 8) if n_aes >= 65536 else (256, 1, 4))
+        kname = f"gcm_ragged_staged<{'true' if open_ else 'false'}, true, {wg}, false, {r}, {kl}>"
     pmc = load_pmc("c5", kname)
     result = {
         "metric": "GiB/s device-resident AEAD encrypt+decrypt, mixed 64B-16KiB records per GPU",

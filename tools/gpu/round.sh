@@ -3,7 +3,7 @@
 # rocprofv3 kernel stats of the default bench.  Outputs in gpurun_out/round/.
 set -eu
 R=$GRAFT_REPO_ROOT; cd $R
-O=$R/gpurun_out/round; mkdir -p $O
+O=$R/gpurun_out/${ROUND_DIR:-round}; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/ -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { tail -20 $O/bench_c2.err; exit 1; }
