@@ -733,14 +733,28 @@ NA_DEV void wave_store(const UniformArgs &a, const WaveIO<K> &io, int j0, int la
                        const uint4 *t, uint32_t lane, uint32_t okm)
 {
     const int u = j0 + io.kk;
+#ifdef NA_STORE_AUX
+    /* buffer stores with cache-policy bits NA_STORE_AUX (sc0 = 1, nt = 2,
+       sc1 = 16) from the wave's first record (A/B builds) */
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(io.rq);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + (size_t)r0 * a.out_stride, 0, 0x7FFFFFFF, 0x00020000);
+#endif
     if (u < 0 || u > last_full) return;
     const uint32_t off = io.c16 + 64u * (uint32_t)u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint4 q = t[tile_slot(16u * i + (lane >> 2), lane & 3)];
         const uint32_t r = wave_rec(io, i);
-        if (r < a.n_records && ((okm >> i) & 1))
+        if (r < a.n_records && ((okm >> i) & 1)) {
+#ifdef NA_STORE_AUX
+            const na_u32x4 v = {q.x, q.y, q.z, q.w};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r - r0) * (uint32_t)a.out_stride + off, 0,
+                                                   NA_STORE_AUX);
+#else
             rec_store16(a.out + (size_t)r * a.out_stride + off, q);
+#endif
+        }
     }
 }
 
