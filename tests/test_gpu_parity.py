@@ -183,34 +183,42 @@ def test_uniform_staged_kernels(aead, gpu, oracle, cipher):
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L]), f"len={L} rec={i}"
 
 
-@pytest.mark.parametrize("cipher,lanes,rps", [(CHACHA, 4, 256), (CHACHA, 4, 13), (CHACHA, 8, 256),
-                                              (CHACHA, 8, 13), (CHACHA, 1, 16), (AES, 0, 256),
-                                              (AES, 0, 13)])
-def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes, rps):
+@pytest.mark.parametrize("cipher,lanes,rps,adl", [(CHACHA, 4, 256, 0), (CHACHA, 4, 13, 0),
+                                                  (CHACHA, 8, 256, 0), (CHACHA, 8, 13, 0),
+                                                  (CHACHA, 1, 16, 0), (AES, 0, 256, 0),
+                                                  (AES, 0, 13, 0), (CHACHA, 4, 256, 21),
+                                                  (AES, 0, 256, 21)])
+def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes, rps, adl):
     """Open in place (in == out, one stride): every verified record becomes
     its plaintext and every rejected one reads exactly as given — CT and tag
-    bytes — including in the single-pass staged ChaChaPoly kernels, which
-    write plaintext before the verdict and re-encrypt on failure."""
+    bytes — including in the single-pass staged kernels (ChaChaPoly and
+    AES-GCM), which write plaintext before the verdict and re-encrypt on
+    failure; with and without associated data."""
     torch = _torch()
-    rng = np.random.default_rng(808 + lanes + rps + (cipher & 3))
+    rng = np.random.default_rng(808 + lanes + rps + (cipher & 3) + adl)
     for L, count in [(1400, 700), (0, 70), (17, 300), (4096, 40), (100, 257)]:
         S = (count + rps - 1) // rps
         keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
         nb = rng.integers(0, 2**62, S, dtype=np.uint64)
         stride_ = (L + 16 + 63) // 64 * 64
         pt = rng.integers(0, 256, count * stride_ + 64, dtype=np.uint8)
-        ct = oracle_seal_records(oracle, cipher, keys, nb, rps, pt, stride_, L, count, stride_)
+        ad = rng.integers(0, 256, count * 32 + 64, dtype=np.uint8)
+        akw = dict(ad=ad, ad_stride=32, ad_len=adl) if adl else {}
+        ct = oracle_seal_records(oracle, cipher, keys, nb, rps, pt, stride_, L, count, stride_, **akw)
         bad = sorted(set(int(x) for x in rng.integers(0, count, 9)))
         for b in bad:
             ct[b * stride_ + int(rng.integers(0, L + 16))] ^= 0x21
         ctx, _k = prepare(aead, cipher, keys)
         d_nb = dev(nb.view(np.int64))
         d_buf = dev(ct)
+        d_ad = dev(ad)
         d_st = torch.full((count,), 7, dtype=torch.uint8, device="cuda")
         assert aead.dev_uniform(True, cipher, ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(),
                                 inp=d_buf.data_ptr(), out=d_buf.data_ptr(), in_stride=stride_,
                                 out_stride=stride_, length=L, n_records=count, recs_per_state=rps,
-                                status=d_st.data_ptr(), lanes=lanes, stream=stream()) == 0
+                                status=d_st.data_ptr(), lanes=lanes, stream=stream(),
+                                ad=d_ad.data_ptr() if adl else 0, ad_stride=32 if adl else 0,
+                                ad_len=adl) == 0
         sync()
         back, st = d_buf.cpu().numpy(), d_st.cpu().numpy()
         for i in range(count):
@@ -479,7 +487,9 @@ def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, lanes, fast
     tampered = sealed.copy()
     for i in np.nonzero(bad)[0]:
         o, L = int(offs[i]), int(lens[i])
-        tampered[o + L + int(rng.integers(0, 16))] ^= 0x40
+        # ciphertext or tag byte: the single-pass opens write plaintext before
+        # the verdict and must give back exactly these bytes in place
+        tampered[o + int(rng.integers(0, L + 16))] ^= 0x40
     d_buf = dev(tampered)
     d_st = torch.full((count,), 9, dtype=torch.uint8, device="cuda")
     assert aead.dev_ragged(True, cipher, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
