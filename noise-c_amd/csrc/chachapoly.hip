@@ -304,6 +304,27 @@ NA_DEV void poly_close(Fe acc, int k, const Mul &mr, const Mul &mfinal, uint64_t
     fe_finish(acc, s, tag);
 }
 
+/* The key stream of lane slot v of a staged step.  Slots before block 0
+   (v < 0: the end alignment's padding, 1 of 24 at 1400 B, 3 of 20 at 1024 B)
+   carry no block, and their lanes run the step switched off instead of
+   computing a block no one reads.  The issue slots are the same; what it
+   saves is energy, and the chip holds its clock by energy under this load
+   (MI355X_MICROARCH.md, DVFS give-back): C4 +1.1 %, perf +0.9 % in three
+   interleaved rounds (profiles/r02/mask_idle_ab.jsonl).  -DNA_NO_MASK_IDLE
+   restores the unmasked step for A/B runs. */
+NA_DEV void slot_block(const uint32_t key[8], const ChaPre &pre, int v, uint32_t n_lo,
+                       uint32_t n_hi, uint32_t x[16])
+{
+#ifndef NA_NO_MASK_IDLE
+    if (v < 0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = 0;
+        return;
+    }
+#endif
+    chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+}
+
 template <int K, bool FAST>
 NA_DEV void seal_il(const RecView &rv, int k)
 {
@@ -332,7 +353,7 @@ NA_DEV void seal_il(const RecView &rv, int k)
         for (int i = 0; i < 16; ++i) wc[i] = wn[i];
         const int vn = v + K; /* the unit of the next step, loaded now */
         unit_prefetch<FAST>(rv.src, m + 1 < g.steps && vn >= 1, (uint32_t)vn - 1, len, wn);
-        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        slot_block(key, pre, v, n_lo, n_hi, x);
         if (m == 0) {
             poly_key_bcast(x, gbase + (int)g.o, r, s);
             mr = mk_mul(r);
@@ -402,7 +423,7 @@ NA_DEV bool open_il_1p(const RecView &rv, int k)
         for (int i = 0; i < 16; ++i) wc[i] = wn[i];
         const int vn = v + K;
         unit_prefetch<true>(rv.src, m + 1 < g.steps && vn >= 1, (uint32_t)vn - 1, len, wn);
-        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        slot_block(key, pre, v, n_lo, n_hi, x);
         if (m == 0) {
             poly_key_bcast(x, gbase + (int)g.o, r, s);
             mr = mk_mul(r);
@@ -440,7 +461,7 @@ NA_DEV bool open_il_1p(const RecView &rv, int k)
     for (uint32_t m = 0; m < g.steps; ++m) {
         const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
         if (v < 1) continue;
-        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        slot_block(key, pre, v, n_lo, n_hi, x);
         uint32_t w[16];
         unit_in<true>(rv.dst, (uint32_t)v - 1, len, w);
 #pragma unroll
@@ -867,7 +888,7 @@ NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
         /* next step's bytes go into the other tile while this one computes */
         if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
-        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        slot_block(key, pre, v, n_lo, n_hi, x);
         if (m == 0) {
             Fe r;
             poly_key_bcast(x, gbase + (int)g.o, r, s);
@@ -947,7 +968,7 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
         __builtin_amdgcn_wave_barrier();
         if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
-        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        slot_block(key, pre, v, n_lo, n_hi, x);
         if (m == 0) {
             Fe r;
             poly_key_bcast(x, gbase + (int)g.o, r, s);
