@@ -257,7 +257,9 @@ def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length, duplex=Fal
         return f"chachapoly_duplex_staged<{lanes}, {'true' if rps % (64 // lanes) == 0 else 'false'}>"
     if cipher == AES:
         c = "true" if ct else "false"
-        return f"gcm_staged<false, {c}>" if fast and rps % 256 == 0 else f"gcm_uniform<false, {c}>"
+        if fast and rps % 256 == 0:
+            return f"gcm_duplex_staged<{c}>" if duplex else f"gcm_staged<false, {c}>"
+        return f"gcm_uniform<false, {c}>"
     if fast and lanes >= 4:
         return f"chachapoly_seal_staged<{lanes}, {'true' if rps % (64 // lanes) == 0 else 'false'}>"
     return f"chachapoly_seal_uniform<{lanes}, {'true' if fast else 'false'}>"
@@ -519,7 +521,7 @@ def main():
     value = payload_step * args.steps / elapsed / GIB
     alg_seal = N * (2 * L + 16 + AD) + len(sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
     kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L, duplex, args.ct_ghash)
-    if kname.startswith("chachapoly_duplex"):
+    if "_duplex_" in kname:
         # the one launch of a step: one seal + one open of N records each
         alg_launch, launch_ms_ = 2 * alg_seal, launch_ms
     elif not duplex and not per_step:

@@ -332,6 +332,21 @@ int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform
             return hip_rc(hipGetLastError());
         }
     }
+    if (cipher_id == NOISE_CIPHER_AESGCM && sj->n_records && oj->n_records &&
+        !(sj->lanes_per_record && sj->lanes_per_record != GCM_LANES) &&
+        !(oj->lanes_per_record && oj->lanes_per_record != GCM_LANES) &&
+        uniform_fast(sj, false) && uniform_fast(oj, true) &&
+        sj->recs_per_state % GCM_WG_RECS == 0 && oj->recs_per_state % GCM_WG_RECS == 0 &&
+        ct_ghash(sj->flags) == ct_ghash(oj->flags)) {
+        rc = hip_rc(ensure_aes_tables((hipStream_t)stream));
+        if (rc) return rc;
+        UniformArgs a = to_args(sj), b = to_args(oj);
+        const uint32_t sb = (sj->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
+        const uint32_t ob = (oj->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
+        hipLaunchKernelGGL(ct_ghash(sj->flags) ? gcm_duplex_staged<true> : gcm_duplex_staged<false>,
+                           dim3(sb + ob), dim3(GCM_WG), 0, (hipStream_t)stream, a, b, sb, ob);
+        return hip_rc(hipGetLastError());
+    }
     rc = run_uniform(cipher_id, sj, stream, false);
     if (!rc) rc = run_uniform(cipher_id, oj, stream, true);
     return rc;

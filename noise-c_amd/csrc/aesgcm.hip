@@ -670,13 +670,14 @@ NA_DEV uint32_t blk_mask(uint32_t nb, int w)
     return rb >= 4 ? 0xffffffffu : (rb <= 0 ? 0u : ((1u << (8 * rb)) - 1u));
 }
 
+/* One 1024-thread workgroup of a uniform staged job: records
+   [blk * 256, blk * 256 + 256). */
 template <bool OPEN, bool CT>
-__global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
+NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
 {
     constexpr int K = GCM_LANES;
-    __shared__ GcmLds L;
     const uint8_t *TE = (const uint8_t *)&L.te[0][0][0];
-    const uint32_t rec0 = blockIdx.x * (uint32_t)GCM_WG_RECS;
+    const uint32_t rec0 = blk * (uint32_t)GCM_WG_RECS;
     const uint32_t st = rec0 / a.rps; /* one state per workgroup (host-checked) */
     const AesCtx *ctx = (const AesCtx *)a.keys + st;
     gcm_lds_fill(L, ctx);
@@ -784,6 +785,37 @@ __global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
         if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
         else store16(dst + 16 * d, nb, x);
     }
+}
+
+template <bool OPEN, bool CT>
+__global__ __launch_bounds__(GCM_WG) void gcm_staged(UniformArgs a)
+{
+    __shared__ GcmLds L;
+    gcm_staged_wg<OPEN, CT>(a, L, blockIdx.x);
+}
+
+/* Duplex: one launch sealing uniform job s and opening job o (the
+   ChaChaPoly duplex of chachapoly.hip), workgroups alternating between the
+   two while both have some left.  A uniform C3-sized job is 256 workgroups,
+   one per CU, each holding its CU until its slowest wave ends; in one launch
+   the second job's workgroups fill the CUs the first job's leave. */
+template <bool CT>
+__global__ __launch_bounds__(GCM_WG) void gcm_duplex_staged(UniformArgs s, UniformArgs o,
+                                                             uint32_t s_blocks, uint32_t o_blocks)
+{
+    __shared__ GcmLds L;
+    const uint32_t n = min(s_blocks, o_blocks);
+    uint32_t b = blockIdx.x;
+    bool open;
+    if (b < 2 * n) {
+        open = b & 1;
+        b >>= 1;
+    } else {
+        open = o_blocks > s_blocks;
+        b -= n;
+    }
+    if (open) gcm_staged_wg<true, CT>(o, L, b);
+    else gcm_staged_wg<false, CT>(s, L, b);
 }
 
 /* ------------------------------ staged ragged (any mix of states / lengths)
