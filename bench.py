@@ -65,7 +65,14 @@ REHEARSE = os.environ.get("NOISE_BENCH_REHEARSE") == "1"
 
 def cpu_if_rehearsal(t):
     return t.cpu() if REHEARSE else t
-IN_ALIGN = 16  # device record strides are padded to 16 B (layout)
+# Device record slots: strides roundup(len, SLOT_ALIGN) / roundup(len + 16,
+# SLOT_ALIGN).  Whole 128-B lines per slot keep a record's first and last
+# lines its own: with 16-B slots (1408 / 1424 B at 1400 B) the open re-read
+# the line shared with the neighbouring record and the tag's line (duplex HBM
+# bytes 1.13x vs 1.10x algorithmic); +0.6-0.8 % at C2/C3/C4 in three
+# interleaved rounds (profiles/r02/align_all_ab.jsonl).  DESIGN.md §3.
+IN_ALIGN = 16
+SLOT_ALIGN = 128
 
 
 def shard(records_per_gpu: int, states: int, rank: int, world: int):
@@ -305,7 +312,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--lanes", type=int, default=0, help="lanes per record (0 = library default)")
     ap.add_argument("--sets", type=int, default=4, help="rotating batch sets (> MALL)")
-    ap.add_argument("--align", type=int, default=IN_ALIGN, choices=(16, 64, 128, 256),
+    ap.add_argument("--align", type=int, default=SLOT_ALIGN, choices=(16, 64, 128, 256),
                     help="record slot alignment of the device batch (strides roundup(len, align), "
                          "roundup(len + 16, align))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
