@@ -507,8 +507,8 @@ def test_ragged_windows_states_and_tamper(aead, gpu, oracle, cipher, lanes, fast
             assert np.array_equal(back[o:o + L], pt[o:o + L]), i
 
 
-@pytest.mark.parametrize("count", [70_000, 140_000])
-def test_ragged_aes_paired_windows(aead, gpu, oracle, count):
+@pytest.mark.parametrize("count,ct", [(70_000, False), (140_000, False), (70_000, True)])
+def test_ragged_aes_paired_windows(aead, gpu, oracle, count, ct):
     """Ragged AES-GCM batches large enough for the paired shapes, where each
     record group runs a long and a short record one after the other
     (gcm_ragged_staged<.., R = 2>): 70 000 records take 256-record windows of
@@ -516,10 +516,12 @@ def test_ragged_aes_paired_windows(aead, gpu, oracle, count):
     4-lane groups.  Per-state runs of 300 records (windows holding 2 and 3
     states), out of place: a sample of records against the oracle, every
     record's round trip, and tampered records rejected with their output
-    zeroed."""
+    zeroed.  ct: the same through the constant-time GHASH (H^8 in the natural
+    domain for the 8-lane groups)."""
     torch = _torch()
-    rng = np.random.default_rng(4711 + count)
+    rng = np.random.default_rng(4711 + count + ct)
     run = 300
+    flags = aead.FLAG_FAST | (aead.FLAG_CT_GHASH if ct else 0)
     S = (count + run - 1) // run
     keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
     ctx, _k = prepare(aead, AES, keys)
@@ -544,7 +546,7 @@ def test_ragged_aes_paired_windows(aead, gpu, oracle, count):
     d_ct = torch.zeros(total, dtype=torch.uint8, device="cuda")
     assert aead.dev_ragged(False, AES, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
                            inp=d_pt.data_ptr(), out=d_ct.data_ptr(), n_records=count,
-                           flags=aead.FLAG_FAST, stream=stream()) == 0
+                           flags=flags, stream=stream()) == 0
     sync()
     ct = d_ct.cpu().numpy()
     for i in list(rng.choice(count, 400, replace=False)) + list(range(0, count, 211)[:40]) + [count - 1]:
@@ -559,7 +561,7 @@ def test_ragged_aes_paired_windows(aead, gpu, oracle, count):
     d_st = torch.full((count,), 9, dtype=torch.uint8, device="cuda")
     assert aead.dev_ragged(True, AES, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
                            inp=d_ct.data_ptr(), out=d_back.data_ptr(), n_records=count,
-                           status=d_st.data_ptr(), flags=aead.FLAG_FAST, stream=stream()) == 0
+                           status=d_st.data_ptr(), flags=flags, stream=stream()) == 0
     sync()
     st, back = d_st.cpu().numpy(), d_back.cpu().numpy()
     assert np.array_equal(st != 0, bad) and set(np.unique(st)) <= {0, 1}
