@@ -42,3 +42,34 @@ def test_host_cpu_counts():
     assert h["usable_cpus"] >= 1
     assert h["physical_cores"] is None or 1 <= h["physical_cores"] <= h["usable_cpus"]
     assert bench.physical_cores([0]) in (None, 1)
+
+
+def test_default_layout_and_kernel_names():
+    """The bench's default record slots (128 B) and the names of the kernels
+    its roofline reads from profiles/traffic_<cfg>.json: every name the
+    default C2/C3/C4/perf lines look up must be in the committed profile,
+    or the line's traffic would silently read null."""
+    assert bench.SLOT_ALIGN == 128
+    assert (bench.stride(1400, 128), bench.stride(1416, 128)) == (1408, 1536)
+    for cfg in ("c2", "c3", "c4", "perf"):
+        c = bench.CONFIGS[cfg]
+        n, s = c["records"], c["states"]
+        ad = c.get("ad", 0)
+        ins, outs = bench.stride(c["len"], 128), bench.stride(c["len"] + 16, 128)
+        k = bench.kernel_name(c["cipher"], n, n // s, 4, ins, outs, c["len"], duplex=True)
+        assert "_duplex_" in k, (cfg, k)
+        prof = bench.load_pmc(cfg, k)
+        assert prof.get("hbm_bytes_per_launch"), (cfg, k)
+        assert ad == 0 or cfg == "perf"
+
+
+def test_c5_profile_names():
+    """C5's dominant kernels as bench.run_mixed names them (the library's
+    gcm_ragged_shape policy at 64 Ki AES records per GPU: 1024 threads, two
+    records per 8-lane group) are in the committed C5 profile."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "traffic_c5.json")) as f:
+        kernels = json.load(f)["kernels"]
+    for open_ in ("true", "false"):
+        assert f"gcm_ragged_staged<{open_}, true, 1024, false, 2, 8>" in kernels
+    assert "chachapoly_open_ragged<4, true>" in kernels
