@@ -792,8 +792,9 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     alg = 2 * g["bytes"] + 16 * g["n"] + 40 * g["states"]
     achieved = alg / (ms * 1e-3) / 1e9
     # the kernel the library dispatches (aead_api.hip run_ragged), as rocprofv3 names it
-    if g["cipher"] == CHACHA:
-        kname = f"chachapoly_{'open' if open_ else 'seal'}_ragged<{args.lanes or 4}, true>"
+    if g["cipher"] == CHACHA:  # run_ragged: 8 lanes below 128 Ki records, else 4
+        k = args.lanes or (8 if g["n"] < 131072 else 4)
+        kname = f"chachapoly_{'open' if open_ else 'seal'}_ragged<{k}, true>"
     else:  # gcm_ragged_shape: (threads, records per group, lanes per record) by batch size
         n_aes = g["n"]
         wg, r, kl = (1024, 2, 4) if n_aes >= 131072 else ((1024, 2, 8) if n_aes >= 65536 else (256, 1, 4))

@@ -366,6 +366,11 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
     a.n_records = job->n_records;
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
+        /* ragged records are often long (C5 mixes 64 B-16 KiB): 8 lanes up to
+           128 Ki records, two generations of waves that even out the mixed
+           lengths (C5's ChaCha kernels -2.5 % seal / -4 % open at 64 Ki
+           records vs 4 lanes, profiles/r02/c5_lanes_ab.jsonl) */
+        if (!job->lanes_per_record && k == 4 && job->n_records < 2u * 65536u) k = 8;
         KernelFn<RaggedArgs> fn =
             chacha_ragged_fn(k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;

@@ -72,4 +72,4 @@ def test_c5_profile_names():
         kernels = json.load(f)["kernels"]
     for open_ in ("true", "false"):
         assert f"gcm_ragged_staged<{open_}, true, 1024, false, 2, 8>" in kernels
-    assert "chachapoly_open_ragged<4, true>" in kernels
+    assert "chachapoly_open_ragged<8, true>" in kernels
