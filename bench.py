@@ -10,10 +10,20 @@ of the sealed batch, both through the C ABI of noise-c_amd
 Inputs are resident in HBM before timing; the batch sets rotate so that the
 working set (> 1 GiB) cannot be served from the 256 MiB Infinity Cache.
 
-Multi-GPU: one process per GPU (torchrun), records sharded by range with no
-data-path collective — each rank seals/opens its own 64 Ki records of the
-global stream (nonce base = rank x records): weak scaling.  Only the timing
-barrier and a max-over-ranks all_reduce use the process group.
+Multi-GPU: one process per GPU, records sharded by range with no data-path
+collective — each rank seals/opens its own 64 Ki records of the global stream
+(nonce base = rank x records): weak scaling.  Only the timing barrier and a
+max-over-ranks all_reduce use the process group.  `--gpus N` without a
+launcher starts the N ranks itself (a child torch.distributed.run over
+127.0.0.1, before anything touches the GPU) and relays rank 0's line; under a
+launcher WORLD_SIZE must equal --gpus.  After the N-rank region rank 0 runs
+the same per-rank work alone (the others wait at a barrier): that in-run
+N = 1 value gives per_gpu_efficiency.
+
+Every run verifies after its timed region: every open status 0, every opened
+record equal to its plaintext, and the records the timed kernels sealed (set 0
+of this rank's shard) hashing to the golden digest of
+tests/golden/shard_digests.json ("verified" in the line).
 
 The CPU baseline is the reference noise-c itself (oracle/_ref/ref_bench: the
 reference's CipherState API compiled from its own sources), timed on this
@@ -304,9 +314,80 @@ def issue_bound(pmc, avg_launch_ms):
             "source": "SQ_INSTS_VALU from the committed PMC profile / live launch time"}
 
 
-def main():
+def launch_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) without a launcher: run this script as N ranks of a
+    child torch.distributed.run on 127.0.0.1 and return its exit status.  The
+    child is started before this process touches the GPU, and this process
+    never execs (MI355X pool rule)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    return subprocess.run(cmd + sys.argv[1:]).returncode
+
+
+def init_dist(world, local, dry_run):
+    import torch.distributed as dist
+    if REHEARSE or dry_run:
+        dist.init_process_group("gloo")
+    else:
+        import torch
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return dist
+
+
+def max_over_ranks(dist, torch, dev, x: float) -> float:
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = cpu_if_rehearsal(t)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def dry_run(args, rank, world):
+    """--dry-run: the N-rank plumbing with no GPU work — self-launch, the
+    process group (gloo), the barrier / max-over-ranks timing and the rank-0
+    line.  For CPU tests of the launcher; it reports no throughput."""
+    import torch
+    dist = init_dist(world, 0, True) if world > 1 else None
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    elapsed = max_over_ranks(dist, torch, None, time.perf_counter() - t0)
+    result = {"metric": "dry run (no GPU work)", "value": None, "unit": "GiB/s", "n_gpus": world,
+              "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / max(1, args.steps),
+              "dry_run": True, "rank_env": {"WORLD_SIZE": os.environ.get("WORLD_SIZE"),
+                                             "MASTER_ADDR": os.environ.get("MASTER_ADDR")}}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def shard_golden(config: str, rank: int, world: int, strong: bool):
+    """The golden sealed-record digest of this rank's set-0 shard
+    (tests/golden/shard_digests.json), or None."""
+    path = os.path.join(ROOT, "tests", "golden", "shard_digests.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        c = json.load(f)["configs"].get(config, {})
+    if strong:
+        return (c.get("world_rank_sealed_sha256", {}).get(str(world)) or [None] * (rank + 1))[rank]
+    d = c.get("rank_sealed_sha256") or []
+    return d[rank] if rank < len(d) else None
+
+
+def parse_args():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher bench.py starts them itself; "
+                         "under one it must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
@@ -316,12 +397,16 @@ def main():
                     help="record slot alignment of the device batch (strides roundup(len, align), "
                          "roundup(len + 16, align))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", action="store_true", help="check every open status after timing")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the after-timing checks (statuses, round trip, golden digest)")
+    ap.add_argument("--verify", action="store_true", help=argparse.SUPPRESS)  # on by default now
     ap.add_argument("--no-xfer", action="store_true",
                     help="skip the N>1 scatter/seal/gather leg (RCCL, SURVEY.md 8e)")
     ap.add_argument("--xfer-reps", type=int, default=5)
+    ap.add_argument("--no-n1", action="store_true",
+                    help="N > 1: skip the in-run N = 1 reference (rank 0 alone) behind per_gpu_efficiency")
     ap.add_argument("--n1-value", type=float, default=None,
-                    help="value of the same config at N = 1: adds per_gpu_efficiency for N > 1")
+                    help="N = 1 value of the same config from another run (overrides the in-run one)")
     ap.add_argument("--mode", default="duplex", choices=("duplex", "separate"),
                     help="duplex: each step seals one set and opens another in ONE launch "
                          "(noise_aead_dev_duplex_uniform); separate: a seal launch then an open launch")
@@ -332,216 +417,82 @@ def main():
                     help="C2-C4/perf: 2 = consecutive steps alternate between two streams")
     ap.add_argument("--ct-ghash", action="store_true",
                     help="AES-GCM: NOISE_AEAD_FLAG_CT_GHASH (table-free GHASH)")
+    ap.add_argument("--verify-first", action="store_true",
+                    help="opens with NOISE_AEAD_FLAG_VERIFY_FIRST (authenticate, then decrypt)")
     ap.add_argument("--c5-streams", type=int, default=2, choices=(1, 2),
                     help="C5: 2 = the AES-GCM and ChaChaPoly halves on two streams, concurrently")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / process-group plumbing only, no GPU work (CPU tests)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or 1)
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, rank, world)
 
     import torch
     import noise_aead as A
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if REHEARSE:
         local = 0
     if world > 1:
-        import torch.distributed as dist
         torch.cuda.set_device(local)
-        if REHEARSE:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = init_dist(world, local, False)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     cfg = CONFIGS[args.config]
     if args.config == "c5":
         return run_mixed(args, cfg, A, torch, dev, rank, world, dist)
-    cipher, N, L, S = cfg["cipher"], cfg["records"], cfg["len"], cfg["states"]
+    N, S = cfg["records"], cfg["states"]
     if cfg.get("strong"):
         if N % world or S % world:
             raise SystemExit(f"{args.config}: {N} records / {S} states do not split over {world} ranks")
         N, S = N // world, S // world
-    sh = shard(N, S, rank, world)
-    in_stride, out_stride = stride(L, args.align), stride(L + 16, args.align)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
-
-    # keys: SplitMix64 words of seed 0x6B6579 at 4*(global key id)
-    key_ids = torch.tensor(sh["key_ids"], dtype=torch.int64)
-    raw = torch.empty(len(sh["key_ids"]) * 32, dtype=torch.uint8, device=dev)
-    for i, kid in enumerate(sh["key_ids"]):
-        assert A.dev_fill_splitmix(raw[32 * i:].data_ptr(), 32, 0x6B6579, 4 * kid, sp) == 0
-    ctx = torch.empty(len(sh["key_ids"]) * A.dev_ctx_bytes(cipher), dtype=torch.uint8, device=dev)
-    assert A.dev_prepare(cipher, raw.data_ptr(), len(sh["key_ids"]), ctx.data_ptr(), sp) == 0
-    nonce = torch.tensor(sh["nonce_base"], dtype=torch.int64, device=dev)
-    del key_ids
-    AD = cfg.get("ad", 0)
-    ad_buf = None
-    if AD:
-        ad_buf = torch.empty(N * AD, dtype=torch.uint8, device=dev)
-        assert A.dev_fill_splitmix(ad_buf.data_ptr(), ad_buf.numel(), 0x6164, sh["first"] * AD // 8, sp) == 0
-    ad_kw = dict(ad=ad_buf.data_ptr() if AD else 0, ad_stride=AD, ad_len=AD)
-
-    sets = []
-    for b in range(args.sets):
-        pt = torch.empty(N * in_stride, dtype=torch.uint8, device=dev)
-        # plaintext word w of the global stream = splitmix64(seed_pt + w)
-        word0 = (sh["first"] * in_stride + b * (1 << 40)) // 8
-        assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), 0x7074, word0, sp) == 0
-        ct = torch.empty(N * out_stride, dtype=torch.uint8, device=dev)
-        back = torch.empty(N * in_stride, dtype=torch.uint8, device=dev)
-        st = torch.empty(N, dtype=torch.uint8, device=dev)
-        sets.append((pt, ct, back, st))
-    torch.cuda.synchronize(dev)
-
-    lanes = args.lanes or A.dev_default_lanes(cipher, N)
-    jflags = A.FLAG_CT_GHASH if args.ct_ghash else 0
-
-    def seal(b, pt=None, ct=None, stream=sp):
-        if pt is None:
-            pt, ct, _, _ = sets[b]
-        return A.dev_uniform(False, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
-                             inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
-                             out_stride=out_stride, length=L, n_records=N,
-                             recs_per_state=sh["rps"], lanes=lanes, flags=jflags, stream=stream,
-                             **ad_kw)
-
-    def open_(b, stream=sp):
-        _, ct, back, st = sets[b]
-        return A.dev_uniform(True, cipher, ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(),
-                             inp=ct.data_ptr(), out=back.data_ptr(), in_stride=out_stride,
-                             out_stride=in_stride, length=L, n_records=N,
-                             recs_per_state=sh["rps"], status=st.data_ptr(), lanes=lanes,
-                             flags=jflags, stream=stream, **ad_kw)
-
-    # Each step seals set b = s % sets and opens set (s - LAG) % sets, sealed LAG
-    # steps earlier: the ciphertext an open reads was written two full steps
-    # (> 700 MB of traffic) before, so it comes from HBM, not from the 256 MiB
-    # Infinity Cache.  Every set is sealed once before timing, so every open
-    # has ciphertext; a set's ciphertext is the same at every seal.
-    lag = 2 if args.sets >= 3 else 0
-    duplex = args.mode == "duplex"
-
-    def jobs(b, bo, stream):
-        pt, ct, _, _ = sets[b]
-        _, cto, back, st = sets[bo]
-        common = dict(ctx=ctx.data_ptr(), nonce_base=nonce.data_ptr(), length=L, n_records=N,
-                      recs_per_state=sh["rps"], lanes=lanes, flags=jflags, **ad_kw)
-        sj = A.uniform_job(inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=in_stride,
-                           out_stride=out_stride, **common)
-        oj = A.uniform_job(inp=cto.data_ptr(), out=back.data_ptr(), in_stride=out_stride,
-                           out_stride=in_stride, status=st.data_ptr(), **common)
-        return sj, oj
-
-    def step_duplex(b, bo, stream=sp):
-        sj, oj = jobs(b, bo, stream)
-        return A.dev_duplex(cipher, sj, oj, stream)
-
-    # --streams 2 (separate mode): consecutive steps (independent batch sets)
-    # alternate between two streams, so step s+1's seal can start on CUs that
-    # step s's open is leaving.  Set b is reused only every `sets` steps.
-    streams = [stream] + ([torch.cuda.Stream(dev)] if args.streams == 2 and not duplex else [])
-
-    for b in range(args.sets):
-        assert seal(b) == 0
-    for w in range(args.warmup):
-        b, bo = w % args.sets, (w - lag) % args.sets
-        if duplex:
-            assert step_duplex(b, bo) == 0
-        else:
-            assert seal(b) == 0
-            assert open_(bo) == 0
-    torch.cuda.synchronize(dev)
+    wl = UniformWork(args, cfg, A, torch, dev, N, S, shard(N, S, rank, world))
+    elapsed = wl.timed(args.steps, args.warmup, dist)
+    elapsed = max_over_ranks(dist, torch, dev, elapsed)
     if dist:
         dist.barrier()
-    per_step = args.events == "step"
-    if duplex or not per_step:  # launch boundaries (duplex) or just the region's ends
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    else:
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-               torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    if duplex or not per_step:
-        ev[0].record(stream)
-    for s in range(args.steps):
-        b, bo = s % args.sets, (s - lag) % args.sets
-        if duplex or not per_step:
-            if duplex:
-                rc = step_duplex(b, bo)
-            else:
-                st_ = streams[s % len(streams)].cuda_stream
-                rc = seal(b, stream=st_) or open_(bo, stream=st_)
-            if per_step or s == args.steps - 1:
-                ev[s + 1].record(stream)
-            if rc:
-                raise RuntimeError(f"launch failed {rc:#x}")
-            continue
-        st_ = streams[s % len(streams)]
-        ev[s][0].record(st_)
-        rc1 = seal(b, stream=st_.cuda_stream)
-        ev[s][1].record(st_)
-        rc2 = open_(bo, stream=st_.cuda_stream)
-        ev[s][2].record(st_)
-        if rc1 or rc2:
-            raise RuntimeError(f"launch failed {rc1:#x} {rc2:#x}")
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = cpu_if_rehearsal(torch.tensor([elapsed], dtype=torch.float64, device=dev))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        dist.barrier()
+    seal_ms, open_ms = wl.per_direction_ms()
+    verify = None if args.no_verify else wl.verify(args.config, rank, world)
 
-    if duplex or not per_step:
-        # average launch interval over the timed region, gaps included
-        launch_ms = ev[0].elapsed_time(ev[args.steps]) / args.steps / (1 if duplex else 2)
-    else:
-        seal_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
-        open_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / args.steps
-    if duplex or not per_step or len(streams) > 1:
-        # per-direction launch times (separate kernels) from a serial, untimed pass
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        reps = 5
-        e[0].record(stream)
-        for r in range(reps):
-            seal(r % args.sets)
-        e[1].record(stream)
-        for r in range(reps):
-            open_((r - lag) % args.sets)
-        e[2].record(stream)
-        torch.cuda.synchronize(dev)
-        seal_ms = e[0].elapsed_time(e[1]) / reps
-        open_ms = e[1].elapsed_time(e[2]) / reps
-
-    ok = True
-    if args.verify:
-        for b in range(args.sets):
-            pt, _, back, st = sets[b]
-            ok &= bool((st == 0).all().item())
-            v = pt.view(N, in_stride)[:, :L]
-            ok &= bool(torch.equal(back.view(N, in_stride)[:, :L], v))
-
+    L, AD = wl.L, wl.AD
     payload_step = 2.0 * N * L * world                         # both directions, all ranks
     value = payload_step * args.steps / elapsed / GIB
-    alg_seal = N * (2 * L + 16 + AD) + len(sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
-    kname = kernel_name(cipher, N, sh["rps"], lanes, in_stride, out_stride, L, duplex, args.ct_ghash)
-    if "_duplex_" in kname:
+    alg_seal = N * (2 * L + 16 + AD) + len(wl.sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
+    # a VERIFY_FIRST open never shares the duplex launch: two launches a step
+    two_launch = wl.duplex and args.verify_first
+    kname = kernel_name(wl.cipher, N, wl.sh["rps"], wl.lanes, wl.in_stride, wl.out_stride, L,
+                        wl.duplex and not two_launch, args.ct_ghash)
+    if two_launch:
+        alg_launch, launch_ms_ = alg_seal, wl.launch_ms / 2
+    elif "_duplex_" in kname:
         # the one launch of a step: one seal + one open of N records each
-        alg_launch, launch_ms_ = 2 * alg_seal, launch_ms
-    elif not duplex and not per_step:
+        alg_launch, launch_ms_ = 2 * alg_seal, wl.launch_ms
+    elif not wl.duplex and not wl.per_step:
         # seal and open alternate: the mean interval per launch, gaps included
-        alg_launch, launch_ms_ = alg_seal, launch_ms
+        alg_launch, launch_ms_ = alg_seal, wl.launch_ms
     else:
         alg_launch, launch_ms_ = alg_seal, seal_ms
     achieved = alg_launch / (launch_ms_ * 1e-3) / 1e9
     pmc = load_pmc(args.config, kname, 1.0 / world if cfg.get("strong") else 1.0)
     traffic = pmc.get("hbm_bytes_per_launch")
+    S_all = S * world
     result = {
         "metric": (f"GiB/s device-resident AEAD encrypt+decrypt, {N * world // 1024}Ki x {L}B "
-                   f"records in total over {S * world} CipherStates, sharded by state"
+                   f"records in total over {S_all} CipherStates, sharded by state"
                    if cfg.get("strong") else
                    f"GiB/s device-resident AEAD encrypt+decrypt, {N // 1024}Ki x {L}B records"
                    + (f" + {AD}B AD" if AD else "") + " per GPU"),
@@ -557,11 +508,15 @@ def main():
         "dtype": "u32",
         "data": "synthetic (SplitMix64 plaintext and keys, SURVEY.md 8d), resident in HBM",
         "config": {"workload": cfg["workload"], "config": args.config, "records_per_gpu": N,
-                   "record_len": L, "states_per_gpu": S, "lanes_per_record": lanes,
-                   "in_stride": in_stride, "out_stride": out_stride,
+                   "record_len": L, "states_per_gpu": S, "lanes_per_record": wl.lanes,
+                   "in_stride": wl.in_stride, "out_stride": wl.out_stride,
                    "payload_bytes_per_step": int(payload_step), "parallelism": f"records x{world}",
-                   "streams": len(streams), "mode": args.mode, "events": args.events,
-                   "open_reads_set_sealed_steps_before": lag,
+                   "streams": len(wl.streams), "mode": args.mode, "events": args.events,
+                   "open_reads_set_sealed_steps_before": wl.lag,
+                   "open_order": ("verify-first (NOISE_AEAD_FLAG_VERIFY_FIRST: authenticate, then "
+                                  "decrypt verified records)" if args.verify_first else
+                                  "one pass (decrypt while authenticating; a rejected record's "
+                                  "plaintext is undone before the kernel ends)"),
                    **({"ct_ghash": True} if args.ct_ghash else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -573,14 +528,17 @@ def main():
         "open_gibs": round(N * L * world / (open_ms * 1e-3) / GIB, 2),
         "open_roofline_frac": round(alg_seal / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
     }
-    if args.verify:
-        result["verified"] = ok
+    if verify is not None:
+        result["verified"] = verify.pop("ok")
+        result["verify"] = verify
     if world > 1 and not args.no_xfer:
         try:  # reported beside the value; a failure here never voids the bench line
             result["scatter_gather"] = xfer_leg(args, torch, dist, dev, A, rank, world, N, L,
-                                                in_stride, out_stride, sh, sets, seal)
+                                                wl.in_stride, wl.out_stride, wl.sh, wl.sets, wl.seal)
         except Exception as e:
             result["scatter_gather"] = {"error": repr(e)}
+    if world > 1 and not args.no_n1 and args.n1_value is None:
+        result["n1_in_run"] = n1_reference(args, cfg, A, torch, dev, rank, dist, wl, N, S, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(cfg)
@@ -589,14 +547,234 @@ def main():
     finish(args, result, rank, world, dist)
 
 
+class UniformWork:
+    """One rank's uniform workload (C2, C3, C4, perf): keys, the rotating
+    batch sets, the step (one duplex launch, or a seal then an open), the
+    timed region and the after-timing checks."""
+
+    def __init__(self, args, cfg, A, torch, dev, N, S, sh):
+        self.args, self.A, self.torch, self.dev = args, A, torch, dev
+        self.cipher, self.N, self.S, self.sh = cfg["cipher"], N, S, sh
+        self.L = L = cfg["len"]
+        self.in_stride, self.out_stride = stride(L, args.align), stride(L + 16, args.align)
+        self.stream = torch.cuda.current_stream(dev)
+        sp = self.sp = self.stream.cuda_stream
+        cipher = self.cipher
+        # keys: SplitMix64 words of seed 0x6B6579 at 4*(global key id) (SURVEY §8d)
+        raw = torch.empty(len(sh["key_ids"]) * 32, dtype=torch.uint8, device=dev)
+        for i, kid in enumerate(sh["key_ids"]):
+            assert A.dev_fill_splitmix(raw[32 * i:].data_ptr(), 32, SEED_KEY, 4 * kid, sp) == 0
+        self.ctx = torch.empty(len(sh["key_ids"]) * A.dev_ctx_bytes(cipher), dtype=torch.uint8, device=dev)
+        assert A.dev_prepare(cipher, raw.data_ptr(), len(sh["key_ids"]), self.ctx.data_ptr(), sp) == 0
+        self.nonce = torch.tensor(sh["nonce_base"], dtype=torch.int64, device=dev)
+        self.AD = AD = cfg.get("ad", 0)
+        self.ad_buf = None
+        if AD:
+            self.ad_buf = torch.empty(N * AD, dtype=torch.uint8, device=dev)
+            assert A.dev_fill_splitmix(self.ad_buf.data_ptr(), self.ad_buf.numel(), 0x6164,
+                                       sh["first"] * AD // 8, sp) == 0
+        self.ad_kw = dict(ad=self.ad_buf.data_ptr() if AD else 0, ad_stride=AD, ad_len=AD)
+        self.sets = []
+        for b in range(args.sets):
+            pt = torch.empty(N * self.in_stride, dtype=torch.uint8, device=dev)
+            # plaintext word w of the global stream = splitmix64(seed_pt + w)
+            word0 = (sh["first"] * self.in_stride + b * (1 << 40)) // 8
+            assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), SEED_PT, word0, sp) == 0
+            ct = torch.empty(N * self.out_stride, dtype=torch.uint8, device=dev)
+            back = torch.empty(N * self.in_stride, dtype=torch.uint8, device=dev)
+            st = torch.full((N,), 0xFF, dtype=torch.uint8, device=dev)
+            self.sets.append((pt, ct, back, st))
+        torch.cuda.synchronize(dev)
+        self.lanes = args.lanes or A.dev_default_lanes(cipher, N)
+        self.sflags = A.FLAG_CT_GHASH if args.ct_ghash else 0
+        self.oflags = self.sflags | (A.FLAG_VERIFY_FIRST if args.verify_first else 0)
+        # Each step seals set b = s % sets and opens set (s - LAG) % sets, sealed
+        # LAG steps earlier: the ciphertext an open reads was written two full
+        # steps (> 700 MB of traffic) before, so it comes from HBM, not from the
+        # 256 MiB Infinity Cache.  Every set is sealed once before timing, so
+        # every open has ciphertext; a set's ciphertext is the same at every seal.
+        self.lag = 2 if args.sets >= 3 else 0
+        self.duplex = args.mode == "duplex"
+        self.per_step = args.events == "step"
+        # --streams 2 (separate mode): consecutive steps (independent batch
+        # sets) alternate between two streams, so step s+1's seal can start on
+        # CUs that step s's open is leaving.  Set b is reused every `sets` steps.
+        self.streams = [self.stream] + ([torch.cuda.Stream(dev)]
+                                        if args.streams == 2 and not self.duplex else [])
+        self.opened = set()
+
+    def _common(self):
+        return dict(ctx=self.ctx.data_ptr(), nonce_base=self.nonce.data_ptr(), length=self.L,
+                    n_records=self.N, recs_per_state=self.sh["rps"], lanes=self.lanes, **self.ad_kw)
+
+    def seal(self, b, pt=None, ct=None, stream=None):
+        if pt is None:
+            pt, ct, _, _ = self.sets[b]
+        return self.A.dev_uniform(False, self.cipher, inp=pt.data_ptr(), out=ct.data_ptr(),
+                                  in_stride=self.in_stride, out_stride=self.out_stride,
+                                  flags=self.sflags, stream=stream or self.sp, **self._common())
+
+    def open_(self, b, stream=None):
+        _, ct, back, st = self.sets[b]
+        self.opened.add(b)
+        return self.A.dev_uniform(True, self.cipher, inp=ct.data_ptr(), out=back.data_ptr(),
+                                  in_stride=self.out_stride, out_stride=self.in_stride,
+                                  status=st.data_ptr(), flags=self.oflags,
+                                  stream=stream or self.sp, **self._common())
+
+    def step_duplex(self, b, bo):
+        A = self.A
+        pt, ct, _, _ = self.sets[b]
+        _, cto, back, st = self.sets[bo]
+        self.opened.add(bo)
+        sj = A.uniform_job(inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=self.in_stride,
+                           out_stride=self.out_stride, flags=self.sflags, **self._common())
+        oj = A.uniform_job(inp=cto.data_ptr(), out=back.data_ptr(), in_stride=self.out_stride,
+                           out_stride=self.in_stride, status=st.data_ptr(), flags=self.oflags,
+                           **self._common())
+        return A.dev_duplex(self.cipher, sj, oj, self.sp)
+
+    def timed(self, steps, warmup, dist):
+        """Warm up, then time exactly `steps` steps between barrier +
+        synchronize on both sides; returns this rank's seconds.  Also sets
+        launch_ms (HIP events on the launch stream)."""
+        torch, dev, sets = self.torch, self.dev, self.args.sets
+        for b in range(sets):
+            assert self.seal(b) == 0
+        for w in range(warmup):
+            b, bo = w % sets, (w - self.lag) % sets
+            if self.duplex:
+                assert self.step_duplex(b, bo) == 0
+            else:
+                assert self.seal(b) == 0
+                assert self.open_(bo) == 0
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        per_step = self.per_step
+        if self.duplex or not per_step:  # launch boundaries (duplex) or just the region's ends
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        else:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+                   torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        if self.duplex or not per_step:
+            ev[0].record(self.stream)
+        for s in range(steps):
+            b, bo = s % sets, (s - self.lag) % sets
+            if self.duplex or not per_step:
+                if self.duplex:
+                    rc = self.step_duplex(b, bo)
+                else:
+                    st_ = self.streams[s % len(self.streams)].cuda_stream
+                    rc = self.seal(b, stream=st_) or self.open_(bo, stream=st_)
+                if per_step or s == steps - 1:
+                    for other in self.streams[1:]:  # the end event covers every stream's steps
+                        self.stream.wait_stream(other)
+                    ev[s + 1].record(self.stream)
+                if rc:
+                    raise RuntimeError(f"launch failed {rc:#x}")
+                continue
+            st_ = self.streams[s % len(self.streams)]
+            ev[s][0].record(st_)
+            rc1 = self.seal(b, stream=st_.cuda_stream)
+            ev[s][1].record(st_)
+            rc2 = self.open_(bo, stream=st_.cuda_stream)
+            ev[s][2].record(st_)
+            if rc1 or rc2:
+                raise RuntimeError(f"launch failed {rc1:#x} {rc2:#x}")
+        torch.cuda.synchronize(dev)
+        elapsed = time.perf_counter() - t0
+        self.ev = ev
+        if self.duplex or not per_step:
+            # average launch interval over the timed region, gaps included
+            self.launch_ms = ev[0].elapsed_time(ev[steps]) / steps / (1 if self.duplex else 2)
+        else:
+            self.launch_ms = None
+        return elapsed
+
+    def per_direction_ms(self):
+        """Seal / open launch times: per-step events, or (duplex, ends, two
+        streams) a separate serial, untimed pass of the two kernels."""
+        torch, steps = self.torch, self.args.steps
+        if not (self.duplex or not self.per_step or len(self.streams) > 1):
+            seal_ms = sum(e[0].elapsed_time(e[1]) for e in self.ev) / steps
+            open_ms = sum(e[1].elapsed_time(e[2]) for e in self.ev) / steps
+            return seal_ms, open_ms
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        reps, sets = 5, self.args.sets
+        e[0].record(self.stream)
+        for r in range(reps):
+            self.seal(r % sets)
+        e[1].record(self.stream)
+        for r in range(reps):
+            self.open_((r - self.lag) % sets)
+        e[2].record(self.stream)
+        torch.cuda.synchronize(self.dev)
+        return e[0].elapsed_time(e[1]) / reps, e[1].elapsed_time(e[2]) / reps
+
+    def verify(self, config, rank, world):
+        """After the timed region: every opened set's statuses are 0 and its
+        opened records equal its plaintext; set 0's sealed records (written by
+        the timed kernels) hash to the golden digest of this rank's shard."""
+        import hashlib
+        torch, N, L = self.torch, self.N, self.L
+        torch.cuda.synchronize(self.dev)
+        st_ok = rt_ok = True
+        for b in sorted(self.opened):
+            pt, _, back, st = self.sets[b]
+            st_ok &= bool((st == 0).all().item())
+            rt_ok &= bool(torch.equal(back.view(N, self.in_stride)[:, :L], pt.view(N, self.in_stride)[:, :L]))
+        strong = bool(CONFIGS[config].get("strong"))
+        want = shard_golden(config, rank, world, strong)
+        # the golden plaintext is the SplitMix64 stream over roundup16(len)
+        # slots (tests/golden/gen_shard_digests.py): other slot widths differ
+        if want is not None and self.in_stride == stride(L, 16):
+            ct = self.sets[0][1].view(N, self.out_stride)[:, :L + 16].contiguous().cpu().numpy()
+            got = hashlib.sha256(ct.tobytes()).hexdigest()
+            digest = "match" if got == want else "MISMATCH"
+        else:
+            digest = "no golden for this rank/layout"
+        ok = st_ok and rt_ok and digest != "MISMATCH"
+        return {"ok": ok, "sets_opened": len(self.opened), "statuses_zero": st_ok,
+                "round_trip": rt_ok, "sealed_digest_set0": digest,
+                "golden": "tests/golden/shard_digests.json"}
+
+
+def n1_reference(args, cfg, A, torch, dev, rank, dist, wl, N, S, world):
+    """The N = 1 value of this config measured in the same run: rank 0 runs
+    the per-GPU work alone — its own shard for weak scaling, the whole job
+    (world x its shard) for strong scaling — while the other ranks wait at a
+    barrier.  per_gpu_efficiency = value / (N x this)."""
+    dist.barrier()
+    v = 0.0
+    if rank == 0:
+        if cfg.get("strong"):
+            w1 = UniformWork(args, cfg, A, torch, dev, N * world, S * world,
+                             shard(N * world, S * world, 0, 1))
+            el = w1.timed(args.steps, args.warmup, None)
+            v = 2.0 * N * world * w1.L * args.steps / el / GIB
+            del w1
+        else:
+            el = wl.timed(args.steps, args.warmup, None)
+            v = 2.0 * N * wl.L * args.steps / el / GIB
+    v = max_over_ranks(dist, torch, dev, v)
+    dist.barrier()
+    return round(v, 2)
+
+
 def finish(args, result, rank, world, dist):
     """Per-GPU efficiency when an N = 1 value is given, the
     rehearsal label, then rank 0 prints the one JSON line."""
-    if args.n1_value and world > 1:
+    n1 = args.n1_value or result.get("n1_in_run")
+    if n1 and world > 1:
         # (aggregate GiB/s at N) / (N x GiB/s at N = 1), for weak and strong
         # scaling alike (strong: total work fixed, so this is speedup / N)
-        result["per_gpu_efficiency"] = round(result["value"] / (world * args.n1_value), 4)
-        result["n1_value"] = args.n1_value
+        result["per_gpu_efficiency"] = round(result["value"] / (world * n1), 4)
+        result["n1_value"] = n1
+        result["n1_source"] = ("--n1-value" if args.n1_value else
+                               "in-run: rank 0 alone on the same per-GPU work, other ranks at a barrier")
     if REHEARSE and world > 1:
         # every rank on one GPU, collectives on gloo: exercises the N > 1 code
         # path only; per-kernel rates of ranks sharing a GPU mean nothing
@@ -720,6 +898,8 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                            bytes=int(lay["lens"][idx].sum()), states=len(states)))
     torch.cuda.synchronize(dev)
 
+    oflags = A.FLAG_VERIFY_FIRST if args.verify_first else 0
+
     def launch(g, open_, stream=sp, inp=None, out=None):
         inp = inp if inp is not None else (ct if open_ else pt)
         out = out if out is not None else (back if open_ else ct)
@@ -727,7 +907,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                             recs=g["recs"].data_ptr(), inp=inp.data_ptr(),
                             out=out.data_ptr(), n_records=g["n"],
                             status=g["st"].data_ptr() if open_ else 0, lanes=args.lanes,
-                            flags=A.FLAG_FAST, stream=stream)
+                            flags=A.FLAG_FAST | (oflags if open_ else 0), stream=stream)
 
     # Two streams: the LDS-bound AES-GCM kernel and the VALU-bound ChaChaPoly
     # kernel share the CUs instead of running back to back; the open phase
@@ -753,21 +933,21 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
             join[open_].record(side)
             main_s.wait_event(join[open_])
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
+    def timed(d):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if d:
+            d.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        return time.perf_counter() - t0
+
+    elapsed = max_over_ranks(dist, torch, dev, timed(dist))
     if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = cpu_if_rehearsal(torch.tensor([elapsed], dtype=torch.float64, device=dev))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
         dist.barrier()
     # per-kernel times (separate, untimed pass) for the roofline line
     per = []
@@ -781,11 +961,32 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
             torch.cuda.synchronize(dev)
             per.append((e0.elapsed_time(e1) / 5, g, open_))
     ok = all(bool((g["st"] == 0).all().item()) for g in groups)
-    if args.verify:  # round trip on a sample of records (statuses: all of them, above)
-        rng = np.random.default_rng(rank)
-        for j in rng.choice(R, size=min(512, R), replace=False):
-            o, n = int(lay["off"][j]), int(lay["lens"][j])
-            ok &= bool(torch.equal(back[o:o + n], pt[o:o + n]))
+    verify = None
+    if not args.no_verify:
+        # every record's round trip (a device compare of the whole plaintext
+        # area: the slots' padding is never written by the opens, so compare
+        # record bytes only, as a masked view), and the sealed records of the
+        # timed kernels against the golden digest of this rank's shard
+        import hashlib
+        starts = torch.from_numpy(lay["off"]).to(dev)
+        lens_t = torch.from_numpy(lay["lens"]).to(dev)
+        cov = torch.zeros(lay["total"] + 1, dtype=torch.int32, device=dev)
+        cov.index_add_(0, starts, torch.ones_like(starts, dtype=torch.int32))
+        cov.index_add_(0, starts + lens_t, -torch.ones_like(starts, dtype=torch.int32))
+        mask = torch.cumsum(cov, 0, dtype=torch.int32)[:-1] > 0
+        rt_ok = bool(torch.equal(back[mask], pt[mask]))
+        del mask, cov
+        want = shard_golden("c5", rank, world, False)
+        digest = "no golden for this rank"
+        if want is not None:
+            h = hashlib.sha256()
+            ct_h = ct.cpu().numpy()
+            for o, n in zip(lay["off"].tolist(), lay["lens"].tolist()):
+                h.update(ct_h[o:o + n + 16])
+            digest = "match" if h.hexdigest() == want else "MISMATCH"
+            del ct_h
+        verify = {"ok": ok and rt_ok and digest != "MISMATCH", "statuses_zero": ok, "round_trip": rt_ok,
+                  "sealed_digest": digest, "golden": "tests/golden/shard_digests.json"}
     payload = sum(g["bytes"] for g in groups)
     value = 2.0 * payload * world * args.steps / elapsed / GIB
     ms, g, open_ = max(per, key=lambda x: x[0])
@@ -794,7 +995,8 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     # the kernel the library dispatches (aead_api.hip run_ragged), as rocprofv3 names it
     if g["cipher"] == CHACHA:  # run_ragged: 8 lanes below 128 Ki records, else 4
         k = args.lanes or (8 if g["n"] < 131072 else 4)
-        kname = f"chachapoly_{'open' if open_ else 'seal'}_ragged<{k}, true>"
+        kname = (f"chachapoly_open_ragged<{k}, true, {'true' if args.verify_first else 'false'}>"
+                 if open_ else f"chachapoly_seal_ragged<{k}, true>")
     else:  # gcm_ragged_shape: (threads, records per group, lanes per record) by batch size
         n_aes = g["n"]
         wg, r, kl = (1024, 2, 4) if n_aes >= 131072 else ((1024, 2, 8) if n_aes >= 65536 else (256, 1, 4))
@@ -818,14 +1020,56 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
         "kernels_ms": {(("chacha" if gg["cipher"] == CHACHA else "aes") + ("_open" if o else "_seal")): round(m, 4)
                        for m, gg, o in per},
         "all_tags_verified": ok,
+        "open_order": "verify-first" if args.verify_first else "one pass",
     }
+    if verify is not None:
+        result["verified"] = verify.pop("ok")
+        result["verify"] = verify
     if world > 1 and not args.no_xfer:
         try:  # reported beside the value; a failure here never voids the bench line
             result["scatter_gather"] = xfer_leg_mixed(args, torch, dist, dev, A, rank, world, R, S,
                                                       lay, pt, groups, launch)
         except Exception as e:
             result["scatter_gather"] = {"error": repr(e)}
+    if world > 1 and not args.no_n1 and args.n1_value is None:
+        dist.barrier()  # rank 0 alone on its own shard: the in-run N = 1 value
+        v = 2.0 * payload * args.steps / timed(None) / GIB if rank == 0 else 0.0
+        result["n1_in_run"] = round(max_over_ranks(dist, torch, dev, v), 2)
+        dist.barrier()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline_mixed()
+        except Exception as e:  # reported, never fatal to the GPU number
+            result["cpu_baseline"] = {"error": str(e)}
     finish(args, result, rank, world, dist)
+
+
+def cpu_baseline_mixed(budget_s: float = 12.0):
+    """C5's CPU row: the reference's CipherState API (oracle/_ref/ref_bench
+    mixed) over the C5 length mix (64 B-16 KiB, ChaChaPoly / AESGCM by state
+    parity), encrypt then decrypt+verify, one thread per physical core of
+    this job's CPU share."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+    kind = "reference"
+    if not os.path.exists(ref):
+        ref, kind = os.path.join(ROOT, "oracle", "_build", "port_bench"), "port"
+    if not os.path.exists(ref):
+        return None
+    hc = host_cpu()
+    phys = hc["physical_cores"] or hc["usable_cpus"]
+    threads = max(1, min(phys, hc["usable_cpus"], hc["cpu_share"] or phys))
+    probe = json.loads(subprocess.run([ref, "mixed", "x", "0", "600", "1"], capture_output=True,
+                                      text=True, timeout=120, check=True).stdout)
+    per_thread = max(600, int(600 * budget_s / max(probe["seconds"], 1e-6) / threads))
+    r = json.loads(subprocess.run([ref, "mixed", "x", "0", str(per_thread), str(threads)],
+                                  capture_output=True, text=True, timeout=600, check=True).stdout)
+    return {"value": round(r["gib_per_s"], 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "single_thread": round(probe["gib_per_s"], 4), "ok": r["ok"],
+            "sample": (f"{'noise-c ref backend CipherState API' if kind == 'reference' else 'oracle restatement'}"
+                       f" over the C5 mix (64 B-16 KiB, ChaChaPoly even / AESGCM odd states of 256 "
+                       f"records): {threads} threads x {per_thread} records, each encrypted then "
+                       f"decrypted+verified, wall clock; 1 thread: {probe['gib_per_s']:.3f} GiB/s"),
+            **hc}
 
 
 def xfer_leg_mixed(args, torch, dist, dev, A, rank, world, R, S, lay, pt, groups, launch):

@@ -183,9 +183,23 @@ int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_
  * s = i / recs_per_state and uses nonce nonce_base[s] + i % recs_per_state.
  * seal: in + i*in_stride holds len plaintext bytes; out + i*out_stride
  *       receives CT || tag (len + 16 bytes).
- * open: in + i*in_stride holds CT || tag; out + i*out_stride receives the
- *       len plaintext bytes only when the tag verifies; status[i] = 0 (ok) or
- *       1 (MAC failure, nothing written).  in == out (in place) is allowed.
+ * open: in + i*in_stride holds CT || tag; status[i] = 0 (ok) or 1 (MAC
+ *       failure).  A verified record's len plaintext bytes go to
+ *       out + i*out_stride.  A rejected record, by default:
+ *         - in place: its CT || tag read back exactly as given;
+ *         - out of place: its len output bytes are ZEROED.
+ *       The default opens decrypt as they authenticate (one pass over the
+ *       ciphertext), so until the kernel ends a rejected record's output
+ *       bytes may transiently hold unauthenticated plaintext; the kernel
+ *       undoes it (restores / zeroes) before it completes.  With
+ *       NOISE_AEAD_FLAG_VERIFY_FIRST the open authenticates first and writes
+ *       a record's output only after its tag verified — the order of the
+ *       reference's ref backends (cipher-chachapoly.c:135-141,
+ *       cipher-aesgcm.c:172-188): a rejected record's output is not written
+ *       at all, not even zeroed.
+ * Memory: input and output records must be either exactly in place
+ * (in == out and in_stride == out_stride) or fully disjoint; any partial
+ * overlap is refused with NOISE_ERROR_INVALID_PARAM.
  * lanes_per_record: 0 = automatic; ChaChaPoly 1, 2, 4, 8, 16, 32 or 64 (wider
  * groups cut the latency of small batches of long records); AESGCM 4 (0 lets
  * a ragged batch of at most 512 records run one record per workgroup). */
@@ -202,7 +216,7 @@ typedef struct NoiseAeadUniform {
     uint32_t len;            /* <= 65535 - 16 */
     uint32_t ad_len;
     uint32_t lanes_per_record;
-    uint32_t flags;          /* NOISE_AEAD_FLAG_CT_GHASH (FAST is derived) */
+    uint32_t flags;          /* NOISE_AEAD_FLAG_CT_GHASH, _VERIFY_FIRST (FAST is derived) */
 } NoiseAeadUniform;
 
 int noise_aead_dev_seal_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream);
@@ -212,11 +226,13 @@ int noise_aead_dev_open_uniform(int cipher_id, const NoiseAeadUniform *job, void
  * directions (echo-server.c:377-407 opens what it receives and seals what it
  * sends) or a pipeline sealing one batch while opening an earlier one.  The
  * result is exactly noise_aead_dev_seal_uniform(seal_job) followed by
- * noise_aead_dev_open_uniform(open_job); the jobs must be independent (no
- * record memory of one job may overlap output memory of the other:
- * NOISE_ERROR_INVALID_PARAM).  Either job may have n_records == 0.  When the
- * two jobs cannot share a kernel (AESGCM, unaligned layouts, different lane
- * counts) the library issues the two launches on `stream` instead. */
+ * noise_aead_dev_open_uniform(open_job); the jobs must be independent:
+ * nothing one job writes (its output records, the open job's statuses) may
+ * overlap anything the other job reads (records, AD) or writes, else
+ * NOISE_ERROR_INVALID_PARAM.  Either job may have n_records == 0.  When the
+ * two jobs cannot share a kernel (unaligned layouts, different lane counts,
+ * AESGCM without one state per 256 records, a VERIFY_FIRST open) the library
+ * issues the two launches on `stream` instead. */
 int noise_aead_dev_duplex_uniform(int cipher_id, const NoiseAeadUniform *seal_job,
                                   const NoiseAeadUniform *open_job, void *stream);
 
@@ -249,6 +265,13 @@ typedef struct NoiseAeadRagged {
  * processed: nothing is written and, when status is given, status[i] = 2 —
  * for seal too (status is optional there: 0 sealed, 2 refused).
  *
+ * Open: a rejected record's output is handled as for the uniform open
+ * (restored in place / zeroed out of place, or not written at all under
+ * NOISE_AEAD_FLAG_VERIFY_FIRST).  Each record's input and output ranges must
+ * be identical (in + in_off == out + out_off) or disjoint from every other
+ * record's ranges; the descriptors live in device memory, so this is the
+ * caller's guarantee (not checked).
+ *
  * The caller guarantees, for every record: in + in_off and out + out_off are
  * 16-byte aligned, and the input may be read up to roundup64(max(len, 1))
  * bytes (and holds CT || tag for open).  Enables the straight-line dwordx4 path.  The
@@ -265,6 +288,16 @@ typedef struct NoiseAeadRagged {
  * variable NOISE_AEAD_CT_GHASH=1 before the first call turns it on for every
  * job, including the CipherState and wire paths. */
 #define NOISE_AEAD_FLAG_CT_GHASH 2u
+
+/* Open only: authenticate first, decrypt only a verified record, and write
+ * nothing for a rejected one (the reference's verify-then-decrypt order,
+ * cipher-chachapoly.c:135-141, cipher-aesgcm.c:172-188).  Without it the
+ * FAST-layout opens decrypt in one pass and undo a rejected record's
+ * plaintext before the kernel ends (see the uniform open above).  The host
+ * paths (CipherState API, batch, wire) never expose unverified plaintext
+ * either way: they stage records in library memory and copy out only
+ * verified ones; they set this flag (strict order) by default. */
+#define NOISE_AEAD_FLAG_VERIFY_FIRST 4u
 
 int noise_aead_dev_seal_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);
 int noise_aead_dev_open_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);

@@ -99,17 +99,19 @@ KernelFn<UniformArgs> chacha_staged_fn(bool open, bool ukey)
     return open ? chachapoly_open_staged<K, false> : chachapoly_seal_staged<K, false>;
 }
 
+/* vf: a VERIFY_FIRST open takes the two-pass chachapoly_open_uniform, never
+   the one-pass staged kernel */
 template <bool FAST>
-KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey)
+KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf)
 {
     switch (k) {
     case 1: return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
     case 2: return open ? chachapoly_open_uniform<2, FAST> : chachapoly_seal_uniform<2, FAST>;
     case 4:
-        if (FAST) return chacha_staged_fn<4>(open, ukey);
+        if (FAST && !(open && vf)) return chacha_staged_fn<4>(open, ukey);
         return open ? chachapoly_open_uniform<4, FAST> : chachapoly_seal_uniform<4, FAST>;
     case 8:
-        if (FAST) return chacha_staged_fn<8>(open, ukey);
+        if (FAST && !(open && vf)) return chacha_staged_fn<8>(open, ukey);
         return open ? chachapoly_open_uniform<8, FAST> : chachapoly_seal_uniform<8, FAST>;
     case 16: return open ? chachapoly_open_uniform<16, FAST> : chachapoly_seal_uniform<16, FAST>;
     case 32: return open ? chachapoly_open_uniform<32, FAST> : chachapoly_seal_uniform<32, FAST>;
@@ -119,29 +121,33 @@ KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey)
 }
 
 /* ukey: every wave's 64/k records share one state (see u_key_nonce) */
-KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast, bool ukey)
+KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast, bool ukey, bool vf)
 {
-    return fast ? chacha_uniform_fn_t<true>(k, open, ukey) : chacha_uniform_fn_t<false>(k, open, ukey);
+    return fast ? chacha_uniform_fn_t<true>(k, open, ukey, vf)
+                : chacha_uniform_fn_t<false>(k, open, ukey, vf);
 }
 
-template <bool FAST>
+/* VF: the FAST opens' two-pass (verify-first) instantiation; the generic
+   layouts' opens are two-pass already */
+template <bool FAST, bool VF>
 KernelFn<RaggedArgs> chacha_ragged_fn_t(int k, bool open)
 {
     switch (k) {
     case 1: return open ? chachapoly_open_ragged<1, FAST> : chachapoly_seal_ragged<1, FAST>;
     case 2: return open ? chachapoly_open_ragged<2, FAST> : chachapoly_seal_ragged<2, FAST>;
-    case 4: return open ? chachapoly_open_ragged<4, FAST> : chachapoly_seal_ragged<4, FAST>;
-    case 8: return open ? chachapoly_open_ragged<8, FAST> : chachapoly_seal_ragged<8, FAST>;
-    case 16: return open ? chachapoly_open_ragged<16, FAST> : chachapoly_seal_ragged<16, FAST>;
-    case 32: return open ? chachapoly_open_ragged<32, FAST> : chachapoly_seal_ragged<32, FAST>;
-    case 64: return open ? chachapoly_open_ragged<64, FAST> : chachapoly_seal_ragged<64, FAST>;
+    case 4: return open ? chachapoly_open_ragged<4, FAST, VF> : chachapoly_seal_ragged<4, FAST>;
+    case 8: return open ? chachapoly_open_ragged<8, FAST, VF> : chachapoly_seal_ragged<8, FAST>;
+    case 16: return open ? chachapoly_open_ragged<16, FAST, VF> : chachapoly_seal_ragged<16, FAST>;
+    case 32: return open ? chachapoly_open_ragged<32, FAST, VF> : chachapoly_seal_ragged<32, FAST>;
+    case 64: return open ? chachapoly_open_ragged<64, FAST, VF> : chachapoly_seal_ragged<64, FAST>;
     }
     return nullptr;
 }
 
-KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open, bool fast)
+KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open, bool fast, bool vf)
 {
-    return fast ? chacha_ragged_fn_t<true>(k, open) : chacha_ragged_fn_t<false>(k, open);
+    if (!fast) return chacha_ragged_fn_t<false, false>(k, open);
+    return vf ? chacha_ragged_fn_t<true, true>(k, open) : chacha_ragged_fn_t<true, false>(k, open);
 }
 
 /* FAST layout (chachapoly.hip): 16-B aligned record slots whose input may be
@@ -157,13 +163,25 @@ bool uniform_fast(const NoiseAeadUniform *j, bool open)
     return true;
 }
 
-int check_uniform(const NoiseAeadUniform *j)
+void job_span(const NoiseAeadUniform *j, bool out, bool open, uint64_t &lo, uint64_t &hi);
+
+/* open = the job is an open (its input holds CT || tag).  In-place jobs must
+   be exactly in place (in == out, one stride): records whose input and output
+   spans overlap any other way would race with their neighbours' reads (and a
+   rejected record's scrub would wipe input other records still need). */
+int check_uniform(const NoiseAeadUniform *j, bool open)
 {
     if (!j || !j->ctx || !j->nonce_base || !j->in || !j->out || !j->recs_per_state)
         return NOISE_ERROR_INVALID_PARAM;
     if (j->ad_len && !j->ad) return NOISE_ERROR_INVALID_PARAM;
     if (j->len > NOISE_MAX_PAYLOAD_LEN - 16) return NOISE_ERROR_INVALID_LENGTH;
     if ((uintptr_t)j->ctx & 15) return NOISE_ERROR_INVALID_PARAM;
+    if (j->n_records && !(j->in == j->out && j->in_stride == j->out_stride)) {
+        uint64_t il, ih, ol, oh;
+        job_span(j, false, open, il, ih);
+        job_span(j, true, open, ol, oh);
+        if (il < oh && ol < ih) return NOISE_ERROR_INVALID_PARAM;
+    }
     return NOISE_ERROR_NONE;
 }
 
@@ -184,7 +202,13 @@ UniformArgs to_args(const NoiseAeadUniform *j)
     a.len = j->len;
     a.ad_len = j->ad_len;
     a.balance = 0;
+    a.vf = 0;
     return a;
+}
+
+bool verify_first(const NoiseAeadUniform *j, bool open)
+{
+    return open && (j->flags & NOISE_AEAD_FLAG_VERIFY_FIRST);
 }
 
 /* NOISE_AEAD_FLAG_CT_GHASH, or NOISE_AEAD_CT_GHASH=1 in the environment
@@ -249,14 +273,15 @@ KernelFn<RaggedArgs> gcm_ragged_fn(bool open, bool fast, GcmShape sh)
 
 int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool open)
 {
-    int rc = check_uniform(job);
+    int rc = check_uniform(job, open);
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
     UniformArgs a = to_args(job);
+    a.vf = verify_first(job, open);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
         const bool ukey = k >= 4 && job->recs_per_state % (64u / (uint32_t)k) == 0;
-        KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open), ukey);
+        KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open), ukey, a.vf);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
         /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC): open
            balances its waves' progress (profiles/r01_prio_ab.jsonl); in the
@@ -305,16 +330,64 @@ bool spans_overlap(const NoiseAeadUniform *a, bool a_out, bool a_open,
     return al < bh && bl < ah;
 }
 
+/* [lo, hi) of a job's AD (lo == hi: none) and of its status array */
+void ad_span(const NoiseAeadUniform *j, uint64_t &lo, uint64_t &hi)
+{
+    lo = hi = (uint64_t)(uintptr_t)j->ad;
+    if (j->ad_len && j->n_records) hi = lo + (uint64_t)(j->n_records - 1) * j->ad_stride + j->ad_len;
+}
+
+void status_span(const NoiseAeadUniform *j, uint64_t &lo, uint64_t &hi)
+{
+    lo = hi = (uint64_t)(uintptr_t)j->status;
+    if (j->status) hi = lo + j->n_records;
+}
+
+bool range_hits_output(uint64_t lo, uint64_t hi, const NoiseAeadUniform *j, bool open)
+{
+    if (lo == hi) return false;
+    uint64_t ol, oh;
+    job_span(j, true, open, ol, oh);
+    if (lo < oh && ol < hi) return true;
+    if (open && j->status) {
+        uint64_t sl, sh;
+        status_span(j, sl, sh);
+        if (lo < sh && sl < hi) return true;
+    }
+    return false;
+}
+
 int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform *oj, void *stream)
 {
-    int rc = check_uniform(sj);
-    if (!rc) rc = check_uniform(oj);
+    int rc = check_uniform(sj, false);
+    if (!rc) rc = check_uniform(oj, true);
     if (rc) return rc;
-    /* independent jobs: neither writes what the other reads or writes */
-    if (sj->n_records && oj->n_records &&
-        (spans_overlap(sj, true, false, oj, false, true) || spans_overlap(sj, true, false, oj, true, true) ||
-         spans_overlap(oj, true, true, sj, false, false)))
-        return NOISE_ERROR_INVALID_PARAM;
+    /* independent jobs: nothing one job writes (records, statuses) may overlap
+       anything the other reads (records, AD) or writes */
+    if (sj->n_records && oj->n_records) {
+        uint64_t lo, hi;
+        bool clash = spans_overlap(sj, true, false, oj, false, true) ||
+                     spans_overlap(sj, true, false, oj, true, true) ||
+                     spans_overlap(oj, true, true, sj, false, false);
+        ad_span(oj, lo, hi);
+        clash = clash || range_hits_output(lo, hi, sj, false);
+        ad_span(sj, lo, hi);
+        clash = clash || range_hits_output(lo, hi, oj, true);
+        status_span(oj, lo, hi);
+        clash = clash || range_hits_output(lo, hi, sj, false);
+        if (oj->status) {
+            uint64_t il, ih;
+            job_span(sj, false, false, il, ih);
+            clash = clash || (lo < ih && il < hi);
+        }
+        if (clash) return NOISE_ERROR_INVALID_PARAM;
+    }
+    /* a VERIFY_FIRST open never shares a launch with the one-pass kernels */
+    if (verify_first(oj, true)) {
+        rc = run_uniform(cipher_id, sj, stream, false);
+        if (!rc) rc = run_uniform(cipher_id, oj, stream, true);
+        return rc;
+    }
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY && sj->n_records && oj->n_records) {
         const int ks = sj->lanes_per_record ? (int)sj->lanes_per_record : auto_lanes(sj->n_records, 0);
         const int ko = oj->lanes_per_record ? (int)oj->lanes_per_record : auto_lanes(oj->n_records, 0);
@@ -364,6 +437,7 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
     a.ad = job->ad;
     a.status = job->status;
     a.n_records = job->n_records;
+    a.vf = open && (job->flags & NOISE_AEAD_FLAG_VERIFY_FIRST);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
         /* ragged records are often long (C5 mixes 64 B-16 KiB): 8 lanes up to
@@ -372,7 +446,7 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
            records vs 4 lanes, profiles/r02/c5_lanes_ab.jsonl) */
         if (!job->lanes_per_record && k == 4 && job->n_records < 2u * 65536u) k = 8;
         KernelFn<RaggedArgs> fn =
-            chacha_ragged_fn(k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0);
+            chacha_ragged_fn(k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0, a.vf != 0);
         if (!fn) return NOISE_ERROR_INVALID_PARAM;
         return launch(fn, job->n_records, k, a, s);
     }
@@ -602,9 +676,9 @@ int noise_aead_dev_pad(NoiseRandSnapshot *d_rand, uint8_t *d_payloads, uint64_t 
 {
     if (!d_payloads || (n && !d_orig_lens)) return NOISE_ERROR_INVALID_PARAM;
     hipStream_t s = (hipStream_t)stream;
-    if (n == 0) {
-        if (d_done) return hip_rc(hipMemsetAsync(d_done, 0, sizeof(uint32_t), s));
-        return d_rand ? NOISE_ERROR_NONE : NOISE_ERROR_INVALID_PARAM;
+    if (n == 0) { /* NULL state: INVALID_PARAM on both branches (randstate.c:356-362) */
+        const int rc = d_done ? hip_rc(hipMemsetAsync(d_done, 0, sizeof(uint32_t), s)) : NOISE_ERROR_NONE;
+        return rc ? rc : (d_rand ? NOISE_ERROR_NONE : NOISE_ERROR_INVALID_PARAM);
     }
     if (!d_rand || padding_mode == NOISE_PADDING_ZERO) {
         /* randstate.c:356-362: without a state the padding is zeroed anyway */

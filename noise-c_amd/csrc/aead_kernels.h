@@ -24,6 +24,9 @@ struct UniformArgs {
     uint32_t rps, n_records, len, ad_len;
     uint32_t balance;           /* the whole batch is one resident generation
                                    of waves (aead_device.h prio_by_progress) */
+    uint32_t vf;                /* open: NOISE_AEAD_FLAG_VERIFY_FIRST — authenticate
+                                   first, decrypt only verified records, write
+                                   nothing (not even zeros) for a rejected one */
 };
 
 /* Ragged batch: one descriptor per record (variable lengths, states, AD).
@@ -47,6 +50,7 @@ struct RaggedArgs {
     uint8_t *status;   /* open: per record 0 ok / 1 MAC failure / 2 bad length;
                           seal (optional): 0 / 2 */
     uint32_t n_records;
+    uint32_t vf;       /* as UniformArgs::vf */
 };
 
 /* A ragged descriptor's record longer than NOISE_MAX_PAYLOAD_LEN - 16 bytes

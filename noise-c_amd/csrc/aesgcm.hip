@@ -471,9 +471,9 @@ __global__ __launch_bounds__(256) void gcm_uniform(UniformArgs a)
     rv.nonce = a.nonce_base[st] + (uint64_t)(rec - st * a.rps);
     rv.len = a.len;
     rv.ad_len = a.ad_len;
-    const bool ok = gcm_record<OPEN, CT>(rv, l, te, sb);
+    const bool ok = gcm_record<OPEN, CT>(rv, l, te, sb); /* open: verifies first */
     if (OPEN && l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, GCM_LANES);
+    if (!ok && !a.vf) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, GCM_LANES);
 }
 
 template <bool OPEN, bool CT>
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
     rv.ad_len = d.ad_len;
     const bool ok = gcm_record<OPEN, CT>(rv, l, te, sb);
     if (l == GCM_LANES - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, GCM_LANES);
+    if (!ok && !a.vf) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, GCM_LANES);
 }
 
 /* ---------------------------- staged (uniform FAST, one state per workgroup)
@@ -670,6 +670,31 @@ NA_DEV uint32_t blk_mask(uint32_t nb, int w)
     return rb >= 4 ? 0xffffffffu : (rb <= 0 ? 0u : ((1u << (8 * rb)) - 1u));
 }
 
+/* CTR over one lane's data blocks d = d0, d0 + K, ... < M of a record, src to
+   dst: the decrypt pass of a VERIFY_FIRST open, after the tag verified. */
+template <bool FAST = true>
+NA_DEV void gcm_ctr_lane(const uint8_t *TE, const uint32_t *rk, uint32_t tpl, const AesPre &pre,
+                         const uint8_t *src, uint8_t *dst, uint32_t len, uint32_t d0, uint32_t M,
+                         uint32_t K)
+{
+#pragma unroll 1
+    for (uint32_t d = d0; d < M; d += K) {
+        const uint32_t nb = min(len - 16 * d, 16u);
+        uint32_t x[4], ks[4];
+        if (FAST) {
+            const uint4 v = *(const uint4 *)(src + 16 * d);
+            x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+        } else {
+            load16(src + 16 * d, nb, x);
+        }
+        aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+        if (FAST && nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
+        else store16(dst + 16 * d, nb, x);
+    }
+}
+
 /* One 1024-thread workgroup of a uniform staged job: records
    [blk * 256, blk * 256 + 256). */
 template <bool OPEN, bool CT>
@@ -717,16 +742,19 @@ NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
             const uint32_t nb = min(len - 16 * d, 16u);
             /* CTR for both directions in this one pass: the ciphertext is read
                once (open: GHASH over the block as read, plaintext out now,
-               repaired below if the tag fails) */
-            uint32_t ks[4], y[4];
-            aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
+               repaired below if the tag fails).  VERIFY_FIRST opens only
+               authenticate here and decrypt after the verdict. */
+            if (!OPEN || !a.vf) {
+                uint32_t ks[4], y[4];
+                aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
 #pragma unroll
-            for (int w = 0; w < 4; ++w) y[w] = x[w] ^ ks[w];
-            if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(y[0], y[1], y[2], y[3]);
-            else store16(dst + 16 * d, nb, y);
-            if (!OPEN) {
+                for (int w = 0; w < 4; ++w) y[w] = x[w] ^ ks[w];
+                if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(y[0], y[1], y[2], y[3]);
+                else store16(dst + 16 * d, nb, y);
+                if (!OPEN) {
 #pragma unroll
-                for (int w = 0; w < 4; ++w) x[w] = y[w];
+                    for (int w = 0; w < 4; ++w) x[w] = y[w];
+                }
             }
 #pragma unroll
             for (int w = 0; w < 4; ++w) x[w] &= blk_mask(nb, w);
@@ -765,6 +793,10 @@ NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
     load16(src + len, 16, got);
     const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) == 0;
     if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
+    if (a.vf) { /* verified: decrypt now; rejected: nothing was written */
+        if (ok) gcm_ctr_lane(TE, L.rk, tpl, pre, src, dst, len, (c0 + K - (A % K)) % K, M, K);
+        return;
+    }
     if (ok) return;
     /* MAC failure (taken only for a forged or damaged record): the reference
        verifies before decrypting and leaves the buffer untouched
@@ -842,7 +874,7 @@ struct GcmLdsR {
    input readable to roundup16). */
 template <bool OPEN, bool FAST, bool CT, int KL = GCM_LANES>
 NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint32_t tpl,
-                              const uint32_t *rk, const uint4 *h4)
+                              const uint32_t *rk, const uint4 *h4, bool vf)
 {
     /* KL lanes per record (4, or 8 with the H^8 Horner table): the Horner
        step is H^KL, h4 its multiply table */
@@ -874,16 +906,19 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
                 load16(rv.src + 16 * d, nb, x);
             }
             /* one pass for both directions (gcm_staged): open decrypts as it
-               authenticates and repairs on a MAC failure */
-            uint32_t ks[4], y[4];
-            aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
+               authenticates and repairs on a MAC failure; VERIFY_FIRST opens
+               decrypt after the verdict */
+            if (!OPEN || !vf) {
+                uint32_t ks[4], y[4];
+                aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
 #pragma unroll
-            for (int w = 0; w < 4; ++w) y[w] = x[w] ^ ks[w];
-            if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(y[0], y[1], y[2], y[3]);
-            else store16(rv.dst + 16 * d, nb, y);
-            if (!OPEN) {
+                for (int w = 0; w < 4; ++w) y[w] = x[w] ^ ks[w];
+                if (FAST && nb == 16) *(uint4 *)(rv.dst + 16 * d) = make_uint4(y[0], y[1], y[2], y[3]);
+                else store16(rv.dst + 16 * d, nb, y);
+                if (!OPEN) {
 #pragma unroll
-                for (int w = 0; w < 4; ++w) x[w] = y[w];
+                    for (int w = 0; w < 4; ++w) x[w] = y[w];
+                }
             }
 #pragma unroll
             for (int w = 0; w < 4; ++w) x[w] &= blk_mask(nb, w);
@@ -914,6 +949,10 @@ NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint3
     uint32_t got[4];
     load16(rv.src + len, 16, got);
     const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) == 0;
+    if (vf) {
+        if (ok) gcm_ctr_lane<FAST>(TE, rk, tpl, pre, rv.src, rv.dst, len, (c0 + K - (A % K)) % K, M, K);
+        return ok;
+    }
     if (ok) return true;
     /* MAC failure: in place, the lane's blocks XORed with their key stream
        once more give back the ciphertext as given (the reference leaves the
@@ -951,9 +990,10 @@ NA_DEV const uint4 *horner_tab(const AesCtx *ctx)
 
 template <bool OPEN, bool FAST, bool CT, int KL>
 __device__ __forceinline__ bool gcm_record_global(const GcmView &rv, int l,
-                                                  const uint8_t *TE, uint32_t tpl)
+                                                  const uint8_t *TE, uint32_t tpl, bool vf)
 {
-    return gcm_record_staged<OPEN, FAST, CT, KL>(rv, l, TE, tpl, rv.ctx->rk, horner_tab<KL>(rv.ctx));
+    return gcm_record_staged<OPEN, FAST, CT, KL>(rv, l, TE, tpl, rv.ctx->rk, horner_tab<KL>(rv.ctx),
+                                                 vf);
 }
 
 /* WG threads per workgroup (1024, or 256 for batches too small to give
@@ -1018,12 +1058,13 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
         rv.ad_len = d.ad_len;
         bool ok;
         const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
+        const bool vf = OPEN && a.vf;
         if (sl >= 0)
-            ok = gcm_record_staged<OPEN, FAST, CT, KL>(rv, l, TE, tpl, L.rk[sl], L.h4[sl]);
+            ok = gcm_record_staged<OPEN, FAST, CT, KL>(rv, l, TE, tpl, L.rk[sl], L.h4[sl], vf);
         else /* a third state in the window: its own context, from global memory */
-            ok = gcm_record_global<OPEN, FAST, CT, KL>(rv, l, TE, tpl);
+            ok = gcm_record_global<OPEN, FAST, CT, KL>(rv, l, TE, tpl, vf);
         if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-        if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, K);
+        if (!ok && !vf) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)l, K);
     }
 }
 
@@ -1124,7 +1165,7 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
     if (OPEN) {
         __syncthreads();
         if (!verdict) { /* nothing decrypted */
-            scrub_rejected(dst, src, len, t, 256);
+            if (!a.vf) scrub_rejected(dst, src, len, t, 256);
             return;
         }
         for (uint32_t b = t; b < M; b += 256) {

@@ -34,9 +34,13 @@
  * in the loop; only the record's last unit and the tag take an exact-size
  * path, after the loop.  The generic path accepts any alignment.
  *
- * Decrypt verifies first, then decrypts; a record whose tag fails writes
- * nothing (cipher-chachapoly.c:139-141).  The ciphertext is read twice; the
- * second read is served by L2.
+ * Decrypt comes in two forms.  The two-pass opens (open_il, open_ct)
+ * verify first, then decrypt; a record whose tag fails writes nothing
+ * (cipher-chachapoly.c:139-141) and the second ciphertext read is served by
+ * L2.  The one-pass opens (open_il_1p, open_il_staged: the default of the
+ * FAST layouts) decrypt as they authenticate and undo the plaintext of a
+ * rejected record before the kernel ends (restored in place, zeroed out of
+ * place); NOISE_AEAD_FLAG_VERIFY_FIRST selects the two-pass form.
  */
 #include "aead_device.h"
 #include "aead_kernels.h"
@@ -1338,13 +1342,17 @@ __global__ __launch_bounds__(256) void chachapoly_open_uniform(UniformArgs a)
     if (rec >= a.n_records) return;
     const int k = (int)(gtid % K);
     const RecView rv = uniform_view(a, rec);
-    const bool ok = open_any<K, FAST>(rv, k);
+    const bool ok = open_any<K, FAST>(rv, k); /* verifies first, then decrypts */
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)k, K);
+    if (!ok && !a.vf) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)k, K);
 }
 
 /* Ragged batches: the workgroup's 256/K records are taken in length order
-   (window_rec), so the records sharing a wave have near-equal lengths. */
+   (window_rec), so the records sharing a wave have near-equal lengths.
+   Open: VF (NOISE_AEAD_FLAG_VERIFY_FIRST) takes the two-pass open_any —
+   authenticate, then decrypt only a verified record, nothing written for a
+   rejected one (cipher-chachapoly.c:135-141) — instead of the one-pass
+   open_il_1p, whose plaintext exists before the verdict. */
 template <int K, bool FAST>
 __global__ __launch_bounds__(256) void chachapoly_seal_ragged(RaggedArgs a)
 {
@@ -1358,7 +1366,7 @@ __global__ __launch_bounds__(256) void chachapoly_seal_ragged(RaggedArgs a)
     if (threadIdx.x % K == K - 1 && a.status) a.status[rec] = 0;
 }
 
-template <int K, bool FAST>
+template <int K, bool FAST, bool VF = false>
 __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
 {
     __shared__ uint32_t order[256 / K];
@@ -1376,7 +1384,7 @@ __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
         ok = open_il<K, true, true>(rv, k, AuthRing{r0[w], r1[w], r2[w]});
     } else
 #else
-    if constexpr (FAST && K >= 4) {
+    if constexpr (FAST && K >= 4 && !VF) {
         ok = open_il_1p<K>(rv, k); /* one pass: the ciphertext is read once */
     } else
 #endif
@@ -1384,7 +1392,7 @@ __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
         ok = open_any<K, FAST>(rv, k);
     }
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-    if (!ok) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)k, K);
+    if (!ok && !VF) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)k, K);
 }
 
 } // namespace na

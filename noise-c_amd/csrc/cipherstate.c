@@ -211,6 +211,8 @@ typedef struct {
     uint64_t nonce;
     size_t idx;        /* caller's record index */
     int skip;          /* in: not dispatched (nonce exhausted) */
+    int forge;         /* in (batch open): tried at the state's current n, as
+                          the record after a MAC failure is */
     int status;        /* out: NOISE_ERROR_NONE / _MAC_FAILURE / _SYSTEM */
     int commit;        /* set by the decide step: copy the result to data */
     int defer;         /* set by the decide step: retry in a later round */
@@ -371,7 +373,10 @@ static int launch_chunk(Staging *sg, const Chunk *c, int ci, int open, int zc)
         job.status = base + c->status_off + first;
         job.n_records = count;
         job.lanes_per_record = k == 0 ? na_chacha_lanes(count, c->chacha_max_len) : na_aes_lanes(count);
-        job.flags = NOISE_AEAD_FLAG_FAST;
+        /* opens verify before they decrypt (cipher-chachapoly.c:135-141,
+           cipher-aesgcm.c:172-188): the staging slot of a rejected record is
+           never written */
+        job.flags = NOISE_AEAD_FLAG_FAST | (open ? NOISE_AEAD_FLAG_VERIFY_FIRST : 0);
         job.reserved_ = 0;
         int cid = k == 0 ? NOISE_CIPHER_CHACHAPOLY : NOISE_CIPHER_AESGCM;
         int rc = open ? noise_aead_dev_open_ragged(cid, &job, sg->stream)
@@ -546,6 +551,7 @@ static int hip_crypt(NoiseCipherState *state, const uint8_t *ad, size_t ad_len,
     j.nonce = state->n; /* the backend reads n; the front end owns n++ */
     j.idx = 0;
     j.skip = 0;
+    j.forge = 0;
     int rc = run_jobs(&j, 1, open, NULL, NULL);
     return rc ? rc : j.status;
 }
@@ -775,6 +781,7 @@ int noise_cipherstate_encrypt_batch(NoiseCipherState *const *states, const uint8
         j->nonce = st->n++; /* advanced even if the backend fails (cipherstate.c:325-326) */
         j->idx = i;
         j->skip = 0;
+        j->forge = 0;
     }
     int rc = run_jobs(jobs, nj, 0, NULL, NULL);
     for (size_t k = 0; k < nj; ++k) {
@@ -791,10 +798,20 @@ typedef struct {
     int *results;
 } OpenBatch;
 
+/* records dispatched, at least, in the first optimistic round after a run of
+   forgeries ended (noise_cipherstate_decrypt_batch) */
+#define FORGE_RESUME 64
+
 /* The sequential semantics of noise_cipherstate_decrypt_with_ad
-   (cipherstate.c:373-410) applied in record order: a MAC failure leaves the
-   record and n untouched, and every later record of that state depends on n,
-   so it is deferred to the next round instead of committed. */
+   (cipherstate.c:373-410) applied in record order.  A MAC failure leaves the
+   record and n untouched, so the next record of the state is tried at the
+   same n.  Each round tests one hypothesis per state:
+     optimistic (forge = 0): records at n, n+1, ... — right up to the first
+       failure, which is final; the records after it rest on a wrong nonce and
+       are deferred;
+     forge (forge = 1 after a failure): every record at n — each failure is
+       final (the sequential call would fail at n too) up to the first record
+       that verifies, which commits; the records after it are deferred. */
 static void open_batch_decide(Job *jobs, size_t lo, size_t hi, void *u)
 {
     OpenBatch *b = (OpenBatch *)u;
@@ -802,11 +819,11 @@ static void open_batch_decide(Job *jobs, size_t lo, size_t hi, void *u)
         Job *j = &jobs[k];
         HipCipherState *st = j->st;
         j->commit = j->defer = 0;
-        if (st->b_failed) {
+        if (st->b_stop) {
             j->defer = 1;
             continue;
         }
-        if (j->skip) { /* nonce exhausted (cipherstate.c:391-397) */
+        if (j->skip) { /* nonce exhausted (cipherstate.c:391-397): final */
             b->results[j->idx] = NOISE_ERROR_INVALID_NONCE;
             continue;
         }
@@ -815,8 +832,9 @@ static void open_batch_decide(Job *jobs, size_t lo, size_t hi, void *u)
             j->commit = 1;
             ++st->parent.n;
             b->buffers[j->idx].size -= 16;
-        } else {
-            st->b_failed = 1;
+            if (j->forge) st->b_stop = st->b_hit = 1; /* the run of forgeries ended */
+        } else if (!j->forge) {
+            st->b_stop = st->b_hit = 1; /* a run of forgeries starts here */
         }
     }
 }
@@ -850,12 +868,15 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
     }
     /* Round 1 validates everything and dispatches every record with the
        nonce it gets if all earlier records of its state verify.  A MAC
-       failure leaves n where it was, so that state's later records are
-       re-run in later rounds with the nonce the sequential calls would have
-       used.  After a failure a state dispatches a window of records per round
-       that restarts at 1 and doubles while they verify: a run of forged
-       records costs one small round each instead of re-running everything
-       after it every time, so the GPU work stays linear in the batch. */
+       failure leaves n where it was, so the state's later records are
+       re-run in later rounds (open_batch_decide): first as a run of
+       forgeries — a window of records all at n, 1 record, then 2, 4, ...
+       while they all fail — then, once one verifies, optimistically again in
+       windows of twice the last forge window (at least FORGE_RESUME) that
+       double while they verify.  A run of k forged records therefore costs
+       O(log k) rounds and the records dispatched stay linear in the batch;
+       k isolated forgeries cost O(k) rounds (each one moves the nonces of
+       every later record). */
     size_t np = 0;
     for (size_t i = 0; i < count; ++i) {
         NoiseCipherState *st = states[i];
@@ -869,6 +890,7 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
         results[i] = check_decrypt(st, ad, ad_len, &buffers[i], &pass);
         if (results[i] || pass) continue;
         ((HipCipherState *)st)->b_window = 0;
+        ((HipCipherState *)st)->b_forge = 0;
         pend[np++] = i;
     }
     OpenBatch ob = {buffers, results};
@@ -882,7 +904,7 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
             if (st->b_epoch != epoch) {
                 st->b_epoch = epoch;
                 st->b_next = st->parent.n;
-                st->b_failed = 0;
+                st->b_stop = st->b_hit = 0;
                 st->b_sent = 0;
             }
             if (st->b_window && st->b_sent >= st->b_window) { /* beyond this round's window */
@@ -898,21 +920,30 @@ int noise_cipherstate_decrypt_batch(NoiseCipherState *const *states, const uint8
             j->data = buffers[i].data;
             j->len = buffers[i].size - 16;
             j->idx = i;
-            /* assumes the earlier records of the state verify; an exhausted
-               nonce stays exhausted (cipherstate.c:391-397) */
-            j->nonce = st->b_next;
-            j->skip = st->b_next == NONCE_LIMIT;
-            if (!j->skip) ++st->b_next;
+            /* optimistic: assumes the earlier records of the state verify;
+               forge: that they fail.  An exhausted nonce stays exhausted
+               (cipherstate.c:391-397) */
+            j->forge = st->b_forge;
+            j->nonce = st->b_forge ? st->parent.n : st->b_next;
+            j->skip = j->nonce == NONCE_LIMIT;
+            if (!j->skip && !st->b_forge) ++st->b_next;
         }
         ++t_batch_rounds;
         t_batch_dispatched += nj;
         rc = run_jobs(jobs, nj, 1, open_batch_decide, &ob);
-        for (size_t k = 0; k < nj; ++k) { /* next round's window of each state */
+        for (size_t k = 0; k < nj; ++k) { /* next round's mode and window of each state */
             HipCipherState *st = jobs[k].st;
             if (st->b_upd == epoch) continue;
             st->b_upd = epoch;
-            if (st->b_failed) st->b_window = 1;
-            else if (st->b_window) st->b_window *= 2;
+            if (!st->b_hit) { /* the hypothesis held for the whole window */
+                if (st->b_window) st->b_window *= 2;
+            } else if (!st->b_forge) { /* optimistic round hit a MAC failure */
+                st->b_forge = 1;
+                st->b_window = 1;
+            } else { /* a forge round found the record that verifies */
+                st->b_forge = 0;
+                st->b_window = st->b_window * 2 > FORGE_RESUME ? st->b_window * 2 : FORGE_RESUME;
+            }
         }
         size_t nnext = 0;
         for (size_t p = 0; p < np; ++p) {

@@ -47,9 +47,12 @@ typedef struct {
     /* scratch for the batch walker (a CipherState is single-owner) */
     uint64_t b_epoch;
     uint64_t b_next;   /* nonce the next record of this batch round will use */
-    int b_failed;
-    uint64_t b_upd;    /* round whose outcome last set b_window */
-    uint64_t b_window; /* records dispatched per round after a MAC failure (0 = all) */
+    int b_stop;        /* this round's later records rest on a wrong nonce guess */
+    int b_forge;       /* round mode: 1 = every record tried at nonce n (a run of
+                          forgeries), 0 = records at n, n+1, ... (all verify) */
+    int b_hit;         /* forge round: a record verified; optimistic round: one failed */
+    uint64_t b_upd;    /* round whose outcome last set b_window / b_forge */
+    uint64_t b_window; /* records dispatched per round (0 = all) */
     uint64_t b_sent;   /* records dispatched in the current round */
 } HipCipherState;
 

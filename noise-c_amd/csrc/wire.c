@@ -153,7 +153,9 @@ static int launch_ragged(int open, const HipCipherState *st, const uint8_t *d_ba
     job.n_records = (uint32_t)n;
     job.lanes_per_record = st->parent.cipher_id == NOISE_CIPHER_CHACHAPOLY
                                ? na_chacha_lanes((uint32_t)n, max_len) : na_aes_lanes((uint32_t)n);
-    job.flags = 0; /* frames sit at 2-byte offsets: the any-alignment kernels */
+    /* frames sit at 2-byte offsets: the any-alignment kernels; opens verify
+       before they decrypt (the reference's order, cipher-chachapoly.c:135-141) */
+    job.flags = open ? NOISE_AEAD_FLAG_VERIFY_FIRST : 0;
     job.reserved_ = 0;
     return open ? noise_aead_dev_open_ragged(st->parent.cipher_id, &job, s)
                 : noise_aead_dev_seal_ragged(st->parent.cipher_id, &job, s);

@@ -16,6 +16,11 @@
  *   perf       tests/performance/test-performance.c:140-179 perf_cipher:
  *              1024 B + 32 B AD encrypt loop, one thread, CPU-time clock,
  *              reports MiB/s.
+ *   mixed      the C5 mix of SURVEY.md §8d as a roundtrip: record i has
+ *              length 64 + splitmix64(0x6C656E + i) % 16321 and belongs to
+ *              state i / 256; even states ChaChaPoly, odd AESGCM (CIPHER and
+ *              LEN are ignored).  Thread t runs records [t*RECORDS,
+ *              (t+1)*RECORDS) with a send/recv CipherState pair per cipher.
  *
  * usage: ref_bench MODE CIPHER LEN RECORDS THREADS   (CIPHER: chachapoly|aesgcm)
  */
@@ -40,7 +45,72 @@ typedef struct {
     int cipher;
     size_t len, records, ad_len;
     int ok;
+    size_t first;      /* mixed: first global record index */
+    double bytes;      /* mixed: payload bytes processed (one direction) */
 } Work;
+
+static uint64_t splitmix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+#define MIX_MAX 16384
+#define MIX_RPS 256
+
+static void *mixed(void *arg)
+{
+    Work *w = (Work *)arg;
+    uint8_t key[32];
+    for (int i = 0; i < 32; ++i) key[i] = (uint8_t)(i * 5 + 3);
+    uint8_t *buf = (uint8_t *)malloc(MIX_MAX + 16);
+    uint8_t *pt = (uint8_t *)malloc(MIX_MAX + 16);
+    for (size_t i = 0; i < MIX_MAX; ++i) pt[i] = (uint8_t)(i * 131 + 7);
+    w->ok = 1;
+    w->bytes = 0;
+#ifdef PORT_ORACLE
+    uint64_t n[2] = {0, 0};
+    const int cid[2] = {CID_CHACHA, CID_AES};
+#else
+    NoiseCipherState *enc[2], *dec[2];
+    const int cid[2] = {CID_CHACHA, CID_AES};
+    for (int c = 0; c < 2; ++c) {
+        noise_cipherstate_new_by_id(&enc[c], cid[c]);
+        noise_cipherstate_new_by_id(&dec[c], cid[c]);
+        noise_cipherstate_init_key(enc[c], key, 32);
+        noise_cipherstate_init_key(dec[c], key, 32);
+    }
+    NoiseBuffer nb;
+#endif
+    for (size_t r = 0; r < w->records; ++r) {
+        const uint64_t i = w->first + r;
+        const size_t len = 64 + (size_t)(splitmix64(0x6C656Eull + i) % 16321u);
+        const int c = (int)((i / MIX_RPS) & 1);
+        memcpy(buf, pt, len);
+#ifdef PORT_ORACLE
+        oracle_aead_encrypt(cid[c], key, n[c], NULL, 0, buf, len);
+        if (oracle_aead_decrypt(cid[c], key, n[c], NULL, 0, buf, len)) w->ok = 0;
+        ++n[c];
+#else
+        noise_buffer_set_inout(nb, buf, len, len + 16);
+        if (noise_cipherstate_encrypt(enc[c], &nb)) w->ok = 0;
+        if (noise_cipherstate_decrypt(dec[c], &nb)) w->ok = 0;
+#endif
+        if (memcmp(buf, pt, len)) w->ok = 0;
+        w->bytes += (double)len;
+    }
+#ifndef PORT_ORACLE
+    for (int c = 0; c < 2; ++c) {
+        noise_cipherstate_free(enc[c]);
+        noise_cipherstate_free(dec[c]);
+    }
+#endif
+    free(buf);
+    free(pt);
+    return NULL;
+}
 
 static double now_mono(void)
 {
@@ -98,7 +168,7 @@ static void *roundtrip(void *arg)
 int main(int argc, char **argv)
 {
     if (argc < 6) {
-        fprintf(stderr, "usage: %s roundtrip|perf chachapoly|aesgcm LEN RECORDS THREADS\n", argv[0]);
+        fprintf(stderr, "usage: %s roundtrip|perf|mixed chachapoly|aesgcm LEN RECORDS THREADS\n", argv[0]);
         return 2;
     }
     const char *mode = argv[1];
@@ -134,6 +204,7 @@ int main(int argc, char **argv)
         return 0;
     }
 
+    const int is_mixed = !strcmp(mode, "mixed");
     Work *ws = (Work *)calloc((size_t)threads, sizeof(Work));
     pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
     for (int t = 0; t < threads; ++t) {
@@ -141,16 +212,25 @@ int main(int argc, char **argv)
         ws[t].len = len;
         ws[t].records = records;
         ws[t].ad_len = 0;
+        ws[t].first = (size_t)t * records;
     }
     double t0 = now_mono();
-    for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, roundtrip, &ws[t]);
+    for (int t = 0; t < threads; ++t) pthread_create(&th[t], NULL, is_mixed ? mixed : roundtrip, &ws[t]);
     int ok = 1;
+    double moved = 0;
     for (int t = 0; t < threads; ++t) {
         pthread_join(th[t], NULL);
         ok &= ws[t].ok;
+        moved += ws[t].bytes;
     }
     double dt = now_mono() - t0;
-    double bytes = 2.0 * (double)len * (double)records * threads;
+    double bytes = is_mixed ? 2.0 * moved : 2.0 * (double)len * (double)records * threads;
+    if (is_mixed) {
+        printf("{\"mode\":\"mixed\",\"records_per_thread\":%zu,\"threads\":%d,\"seconds\":%.6f,"
+               "\"payload_bytes\":%.0f,\"gib_per_s\":%.6f,\"ok\":%s}\n",
+               records, threads, dt, bytes, bytes / dt / (1024.0 * 1024.0 * 1024.0), ok ? "true" : "false");
+        return ok ? 0 : 1;
+    }
     printf("{\"mode\":\"roundtrip\",\"cipher\":\"%s\",\"len\":%zu,\"records_per_thread\":%zu,"
            "\"threads\":%d,\"seconds\":%.6f,\"gib_per_s\":%.6f,\"ok\":%s}\n",
            argv[2], len, records, threads, dt, bytes / dt / (1024.0 * 1024.0 * 1024.0),

@@ -198,8 +198,8 @@ def test_device_api_argument_rules(aead_built):
     The pointers are never dereferenced: every case fails validation."""
     A = aead_built
     fake = 1 << 20  # aligned, non-null, never touched
-    ok = dict(ctx=fake, nonce_base=fake, inp=fake, out=fake, in_stride=1408, out_stride=1424,
-              length=1400, n_records=4, recs_per_state=4)
+    ok = dict(ctx=fake, nonce_base=fake, inp=fake, out=fake + (1 << 30), in_stride=1408,
+              out_stride=1424, length=1400, n_records=4, recs_per_state=4)
     for open_ in (False, True):
         for cid in (A.CHACHAPOLY, A.AESGCM):
             assert A.dev_uniform(open_, cid, **{**ok, "nonce_base": 0}) == A.ERROR_INVALID_PARAM
@@ -216,6 +216,43 @@ def test_device_api_argument_rules(aead_built):
             assert A.dev_ragged(open_, cid, **{**rg, "out": 0}) == A.ERROR_INVALID_PARAM
         assert A.dev_ragged(open_, A.CHACHAPOLY, **{**rg, "lanes": 5}) == A.ERROR_INVALID_PARAM
         assert A.dev_ragged(open_, 0x4399, **rg) == A.ERROR_UNKNOWN_ID
+        # records must be exactly in place or disjoint: in == out
+        # with two strides, or output shifted into the input, is refused
+        for cid in (A.CHACHAPOLY, A.AESGCM):
+            assert A.dev_uniform(open_, cid, **{**ok, "out": fake}) == A.ERROR_INVALID_PARAM
+            assert A.dev_uniform(open_, cid, **{**ok, "out": fake + 64, "out_stride": 1408}) \
+                == A.ERROR_INVALID_PARAM
+            assert A.dev_uniform(open_, cid, **{**ok, "out": fake + 4 * 1408 - 16}) \
+                == A.ERROR_INVALID_PARAM
+
+
+def test_duplex_independence_rules(aead_built):
+    """noise_aead_dev_duplex_uniform refuses jobs one of which writes what the
+    other reads or writes: records, the open job's statuses, either AD
+    (ADVICE r2).  Refused before any HIP call, so no GPU is needed."""
+    A = aead_built
+    G = 1 << 30
+    base = dict(ctx=1 << 20, nonce_base=1 << 20, length=1400, n_records=4, recs_per_state=4)
+    seal = dict(inp=2 * G, out=3 * G, in_stride=1408, out_stride=1536, **base)
+    opn = dict(inp=4 * G, out=5 * G, in_stride=1536, out_stride=1408, status=6 * G, **base)
+    for cid in (A.CHACHAPOLY, A.AESGCM):
+        def duplex(s, o):
+            return A.dev_duplex(cid, A.uniform_job(**s), A.uniform_job(**o))
+        # the open reads the seal's output
+        assert duplex(seal, {**opn, "inp": 3 * G}) == A.ERROR_INVALID_PARAM
+        # outputs overlap
+        assert duplex(seal, {**opn, "out": 3 * G + 100}) == A.ERROR_INVALID_PARAM
+        # the open writes the seal's input
+        assert duplex(seal, {**opn, "out": 2 * G}) == A.ERROR_INVALID_PARAM
+        # the open's statuses land in the seal's output / input
+        assert duplex(seal, {**opn, "status": 3 * G + 1536}) == A.ERROR_INVALID_PARAM
+        assert duplex(seal, {**opn, "status": 2 * G + 8}) == A.ERROR_INVALID_PARAM
+        # the open's AD sits in the seal's output; the seal's AD in the open's output
+        assert duplex(seal, {**opn, "ad": 3 * G, "ad_len": 16, "ad_stride": 16}) == A.ERROR_INVALID_PARAM
+        assert duplex({**seal, "ad": 5 * G + 32, "ad_len": 8, "ad_stride": 8}, opn) \
+            == A.ERROR_INVALID_PARAM
+        # the seal's AD sits in the open's status array
+        assert duplex({**seal, "ad": 6 * G, "ad_len": 8, "ad_stride": 8}, opn) == A.ERROR_INVALID_PARAM
 
 
 STRERROR = {0: "No error", 0x4501: "Out of memory", 0x4502: "Unknown identifier",

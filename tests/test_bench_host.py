@@ -72,4 +72,50 @@ def test_c5_profile_names():
         kernels = json.load(f)["kernels"]
     for open_ in ("true", "false"):
         assert f"gcm_ragged_staged<{open_}, true, 1024, false, 2, 8>" in kernels
-    assert "chachapoly_open_ragged<8, true>" in kernels
+    assert "chachapoly_open_ragged<8, true, false>" in kernels or \
+        "chachapoly_open_ragged<8, true>" in kernels
+
+
+def _bench(args, env=None, timeout=240):
+    import subprocess
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True,
+                          text=True, timeout=timeout, env=e)
+
+
+def test_gpus_n_launches_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher starts the two
+    ranks itself (a child torch.distributed.run on 127.0.0.1, gloo here) and
+    relays rank 0's one line, which reports n_gpus 2.  --dry-run: the
+    launcher and process-group plumbing without GPU work."""
+    r = _bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["dry_run"] and d["rank_env"]["WORLD_SIZE"] == "2"
+    assert d["rank_env"]["MASTER_ADDR"] == "127.0.0.1"
+
+
+def test_gpus_must_match_world_size():
+    r = _bench(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+    r = _bench(["--dry-run", "--steps", "1"])  # no launcher, no --gpus: one rank
+    assert r.returncode == 0 and json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1
+
+
+def test_shard_goldens_cover_every_rank():
+    """bench.py verifies each rank's sealed shard against these digests."""
+    for cfg in ("c2", "c3", "perf", "c5"):
+        for r in range(8):
+            assert bench.shard_golden(cfg, r, 8, False), (cfg, r)
+    for w in (1, 2, 4, 8):
+        for r in range(w):
+            assert bench.shard_golden("c4", r, w, True), (w, r)
+    with open(os.path.join(ROOT, "tests", "golden", "config_digests.json")) as f:
+        base = json.load(f)["configs"]
+    assert bench.shard_golden("c2", 0, 1, False) == base["c2"]["sealed_sha256"]
+    assert bench.shard_golden("c4", 0, 1, True) == base["c4"]["sealed_sha256"]

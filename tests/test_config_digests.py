@@ -139,3 +139,65 @@ def test_full_c5_digest_on_gpu():
     assert hp.hexdigest() == c["pt_sha256"]
     assert hs.hexdigest() == c["sealed_sha256"]
     assert hb.hexdigest() == c["pt_sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_full_size_duplex_at_bench_slots(name):
+    """The kernels bench.py times: C2 / C3 at full size
+    through noise_aead_dev_duplex_uniform at the bench's 128-B record slots
+    (in_stride 1408, out_stride 1536), one state, recs_per_state 65 536 —
+    chachapoly_duplex_staged<4, true> / gcm_duplex_staged<false>.  The seal
+    half's sealed records hash to the golden digest (cipher-chachapoly.c
+    :107-133 / cipher-aesgcm.c:156-170 bytes); the open half, over a batch
+    sealed beforehand with 64 records tampered, accepts every other record
+    with the plaintext digest and rejects (zeroes) exactly the tampered ones."""
+    import torch
+
+    import noise_aead as A
+    A.lib()
+    c = _golden()[name]
+    N, L, cipher = c["records"], c["len"], c["cipher"]
+    ins, outs = 1408, 1536  # bench.py SLOT_ALIGN = 128
+    sp = torch.cuda.current_stream().cuda_stream
+    raw = torch.empty(32, dtype=torch.uint8, device="cuda")
+    assert A.dev_fill_splitmix(raw.data_ptr(), 32, SEED_KEY, 0, sp) == 0
+    ctx = torch.empty(A.dev_ctx_bytes(cipher), dtype=torch.uint8, device="cuda")
+    assert A.dev_prepare(cipher, raw.data_ptr(), 1, ctx.data_ptr(), sp) == 0
+    nb = torch.zeros(1, dtype=torch.int64, device="cuda")
+    pt = torch.empty(N * ins, dtype=torch.uint8, device="cuda")
+    assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), SEED_PT, 0, sp) == 0
+    assert hashlib.sha256(pt.view(N, ins)[:, :L].contiguous().cpu().numpy().tobytes()).hexdigest() \
+        == c["pt_sha256"]
+    common = dict(ctx=ctx.data_ptr(), nonce_base=nb.data_ptr(), length=L, n_records=N,
+                  recs_per_state=N)
+    # batch B: sealed by the separate kernel, then tampered
+    ct_b = torch.empty(N * outs, dtype=torch.uint8, device="cuda")
+    assert A.dev_uniform(False, cipher, inp=pt.data_ptr(), out=ct_b.data_ptr(), in_stride=ins,
+                         out_stride=outs, stream=sp, **common) == 0
+    rng = np.random.default_rng(17 + (cipher & 3))
+    bad = np.unique(rng.integers(0, N, 64))
+    pos = torch.from_numpy(bad * outs + rng.integers(0, L + 16, len(bad))).to("cuda")
+    flat = ct_b.view(-1)
+    flat[pos] ^= 0x40
+    # one duplex launch: seal A (same plaintext) while opening B
+    ct_a = torch.empty(N * outs, dtype=torch.uint8, device="cuda")
+    back = torch.full((N * ins,), 0xA5, dtype=torch.uint8, device="cuda")
+    st = torch.full((N,), 9, dtype=torch.uint8, device="cuda")
+    sj = A.uniform_job(inp=pt.data_ptr(), out=ct_a.data_ptr(), in_stride=ins, out_stride=outs, **common)
+    oj = A.uniform_job(inp=ct_b.data_ptr(), out=back.data_ptr(), in_stride=outs, out_stride=ins,
+                       status=st.data_ptr(), **common)
+    assert A.dev_duplex(cipher, sj, oj, sp) == 0
+    torch.cuda.synchronize()
+    sealed = ct_a.view(N, outs)[:, :L + 16].contiguous().cpu().numpy()
+    assert hashlib.sha256(sealed.tobytes()).hexdigest() == c["sealed_sha256"], name
+    del sealed
+    s = st.cpu().numpy()
+    exp = np.zeros(N, dtype=np.uint8)
+    exp[bad] = 1
+    assert np.array_equal(s, exp), np.nonzero(s != exp)[0][:10]
+    bv, pv = back.view(N, ins)[:, :L], pt.view(N, ins)[:, :L]
+    good = torch.ones(N, dtype=torch.bool, device="cuda")
+    good[torch.from_numpy(bad).to("cuda")] = False
+    assert torch.equal(bv[good], pv[good])
+    assert int(bv[~good].max().item()) == 0  # rejected records zeroed out of place

@@ -4,8 +4,8 @@
   (status 2, nothing written), seal and open, both ciphers;
 - a freed CipherState's device key context reads back as zeros (debug hook:
   NOISE_AEAD_DEBUG_KEEP_FREED keeps the scrubbed allocation alive);
-- a run of forged records in noise_cipherstate_decrypt_batch costs small
-  rounds, not a re-dispatch of everything after each failure, and the results
+- a run of k forged records in noise_cipherstate_decrypt_batch costs
+  O(log k) GPU rounds, the records dispatched stay linear, and the results
   still equal the sequential calls (cipherstate.c:373-410);
 - a state used on two devices is rebuilt on the second (needs 2 GPUs).
 """
@@ -101,43 +101,26 @@ def test_freed_state_context_is_scrubbed(aead, gpu, cipher, monkeypatch):
 
 
 @pytest.mark.parametrize("cipher", [CHACHA, AES])
-def test_forged_run_costs_rounds_not_redispatch(aead, gpu, oracle, cipher):
-    """A state whose batch holds a long run of forged records: results equal
-    the sequential calls, and the records dispatched over all rounds stay
-    linear in the batch (the first version re-ran every later
-    record of the state after each failure, O(n^2))."""
-    rng = np.random.default_rng(5 + (cipher & 3))
+@pytest.mark.parametrize("before,forged,after", [(3, 60, 80), (0, 1000, 5)])
+def test_forged_run_costs_log_rounds(aead, gpu, oracle, cipher, before, forged, after):
+    """A state whose batch holds a run of k forged records: results equal the
+    sequential calls (cipherstate.c:373-410), the run costs O(log k) GPU
+    rounds (forge windows of 1, 2, 4, ... records tried at the same nonce;
+    VERDICT r2 item 6) and the records dispatched stay linear in the batch."""
+    import math
+    from batch_cases import check_against_model, make_records, run_batch
+    rng = np.random.default_rng(5 + (cipher & 3) + forged)
     key = bytes(rng.integers(0, 256, 32, dtype=np.uint8))
-    good_before, forged, good_after = 3, 60, 80
-    records, expect_pt = [], []
-    n = 0
-    for i in range(good_before + forged + good_after):
-        L = int(rng.integers(0, 300))
-        pt = bytes(rng.integers(0, 256, L, dtype=np.uint8))
-        if good_before <= i < good_before + forged:
-            records.append(bytes(rng.integers(0, 256, L + 16, dtype=np.uint8)))  # garbage
-            expect_pt.append(None)
-        else:
-            records.append(oracle.encrypt(cipher, key, n, pt))
-            expect_pt.append(pt)
-            n += 1
+    records = make_records(oracle, cipher, key, [False] * before + [True] * forged + [False] * after,
+                           rng)
     st = aead.CipherState.new_by_id(cipher)[1]
     st.init_key(key)
-    mems = [(C.c_uint8 * len(r)).from_buffer_copy(r) for r in records]
-    bufs = [aead.NoiseBuffer.input(m, len(r)) for m, r in zip(mems, records)]
-    rc, res = aead.decrypt_batch([st] * len(records), bufs)
+    rc, res, mems, bufs, rounds, disp = run_batch(aead, [st] * len(records), records)
     assert rc == 0
-    for i, exp in enumerate(expect_pt):
-        if exp is None:
-            assert res[i] == 0x4504 and bytes(mems[i]) == records[i], i
-        else:
-            assert res[i] == 0 and bytes(mems[i])[:len(exp)] == exp and bufs[i].size == len(exp), i
-    assert st.nonce == n
-    rounds, disp = C.c_uint64(), C.c_uint64()
-    aead.lib().noise_aead_debug_batch_stats(C.byref(rounds), C.byref(disp))
+    check_against_model(oracle, cipher, key, 0, records, res, mems, bufs, st)
     total = len(records)
-    assert disp.value <= 3 * total, (rounds.value, disp.value)
-    assert rounds.value <= forged + 2 + int(np.log2(total)) + 2, (rounds.value, disp.value)
+    assert rounds <= 2 * math.log2(total + 1) + 3, (rounds, disp)
+    assert disp <= 3 * total + 64, (rounds, disp)
     st.free()
 
 

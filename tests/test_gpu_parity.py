@@ -229,21 +229,37 @@ def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes
                 assert st[i] == 0 and np.array_equal(back[o:o + L], pt[o:o + L]), (L, i)
 
 
-@pytest.mark.parametrize("cipher,lanes,layout", [(CHACHA, 4, "fast"), (CHACHA, 8, "fast"),
-                                                 (CHACHA, 4, "packed"), (AES, 0, "fast")])
-def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout):
+FLAG_CT_GHASH, FLAG_VERIFY_FIRST = 2, 4
+DUPLEX_CASES = [((1400, 700, 350), (1400, 300, 100)), ((100, 64, 16), (1401, 513, 513)),
+                ((0, 33, 16), (65, 1000, 16)), ((4096, 5, 5), (17, 0, 1))]
+# one state per 256 records (the AES duplex kernel, the bench's wave-uniform
+# keys) at the bench's 128-B record slots, last workgroup partial
+SLOT_CASES = [((1400, 1024, 512), (1400, 768, 256)), ((1400, 512, 256), (1024, 2048, 1024)),
+              ((1, 256, 256), (1400, 300, 256)), ((1400, 1000, 256), (4096, 256, 256))]
+
+
+@pytest.mark.parametrize("cipher,lanes,layout,flags", [
+    (CHACHA, 4, "fast", 0), (CHACHA, 8, "fast", 0), (CHACHA, 4, "packed", 0), (AES, 0, "fast", 0),
+    (CHACHA, 4, "slot128", 0), (CHACHA, 8, "slot128", 0), (AES, 0, "slot128", 0),
+    (AES, 0, "slot128", FLAG_CT_GHASH), (CHACHA, 4, "slot128", FLAG_VERIFY_FIRST),
+    (AES, 0, "slot128", FLAG_VERIFY_FIRST)])
+def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout, flags):
     """noise_aead_dev_duplex_uniform: seal job A and open job B (other keys,
     nonces, length, record count; some records tampered) in one call must
     equal the two separate calls — i.e. the oracle — byte for byte.  ChaCha
-    FAST layouts run the one-launch duplex kernel, the others two launches."""
+    FAST layouts run the one-launch chachapoly_duplex_staged kernel; AES-GCM
+    with one state per 256 records runs gcm_duplex_staged (plain and CT
+    GHASH); the others, and a VERIFY_FIRST open, two launches.  A rejected
+    record's output is zeroed (one-pass opens) or never written
+    (VERIFY_FIRST)."""
     torch = _torch()
-    rng = np.random.default_rng(3131 + lanes + (cipher & 3) + len(layout))
-    for (La, na, rpsa), (Lb, nb_, rpsb) in [((1400, 700, 350), (1400, 300, 100)),
-                                           ((100, 64, 16), (1401, 513, 513)),
-                                           ((0, 33, 16), (65, 1000, 16)), ((4096, 5, 5), (17, 0, 1))]:
+    rng = np.random.default_rng(3131 + lanes + (cipher & 3) + len(layout) + flags)
+    for (La, na, rpsa), (Lb, nb_, rpsb) in (SLOT_CASES if layout == "slot128" else DUPLEX_CASES):
         def strides(L):
             if layout == "packed":
                 return L, L + 16
+            if layout == "slot128":
+                return (max(L, 1) + 127) // 128 * 128, (L + 16 + 127) // 128 * 128
             return (max(L, 1) + 63) // 64 * 64, (L + 16 + 63) // 64 * 64
         ia, oa = strides(La)
         ib, ob = strides(Lb)
@@ -268,11 +284,12 @@ def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout):
         d_st = torch.full((max(1, nb_),), 7, dtype=torch.uint8, device="cuda")
         sj = aead.uniform_job(ctx=ctxa.data_ptr(), nonce_base=d_nba.data_ptr(), inp=d_pta.data_ptr(),
                               out=d_outa.data_ptr(), in_stride=ia, out_stride=oa, length=La,
-                              n_records=na, recs_per_state=rpsa, lanes=lanes)
+                              n_records=na, recs_per_state=rpsa, lanes=lanes,
+                              flags=flags & FLAG_CT_GHASH)
         oj = aead.uniform_job(ctx=ctxb.data_ptr(), nonce_base=d_nbb.data_ptr(), inp=d_ctb.data_ptr(),
                               out=d_outb.data_ptr(), in_stride=ob, out_stride=ib, length=Lb,
                               n_records=nb_, recs_per_state=rpsb, status=d_st.data_ptr(),
-                              lanes=lanes)
+                              lanes=lanes, flags=flags)
         assert aead.dev_duplex(cipher, sj, oj, stream()) == 0
         sync()
         got_a, back, st = d_outa.cpu().numpy(), d_outb.cpu().numpy(), d_st.cpu().numpy()
@@ -280,7 +297,8 @@ def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout):
         for i in range(nb_):
             seg = back[i * ib: i * ib + Lb]
             if i in bad:
-                assert st[i] == 1 and np.all(seg == 0), f"duplex open len={Lb} rec={i}"
+                fill = 0x5A if flags & FLAG_VERIFY_FIRST else 0
+                assert st[i] == 1 and np.all(seg == fill), f"duplex open len={Lb} rec={i}"
             else:
                 assert st[i] == 0, f"duplex open len={Lb} rec={i}"
                 assert np.array_equal(seg, ptb[i * ib: i * ib + Lb]), f"len={Lb} rec={i}"

@@ -51,6 +51,7 @@ HOST_RULE_TESTS = [
     "tests/test_abi.py::test_strerror_contract",
     "tests/test_abi.py::test_ad_longer_than_descriptor_field_refused",
     "tests/test_wire.py::test_wire_host_rules",
+    "tests/test_batch_host.py",
 ]
 
 
