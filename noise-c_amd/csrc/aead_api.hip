@@ -6,52 +6,16 @@
  * NOISE_ERROR_SYSTEM (constants.h:137), bad arguments to
  * NOISE_ERROR_INVALID_PARAM / _INVALID_LENGTH / _UNKNOWN_ID.
  */
-#include "noise_aead_hip.h"
-#include "aead_kernels.h"
-#include <hip/hip_runtime.h>
-#include <mutex>
+#include "launch.h"
 #include <cstdlib>
 #include <cstring>
 
-
-#include "chachapoly.hip"
-#include "aesgcm.hip"
 #include "kdf.hip"
 #include "pad.hip"
 
 using namespace na;
 
 namespace {
-
-constexpr int kMaxDevices = 64;
-std::mutex g_tab_mu[kMaxDevices];
-bool g_tab_ready[kMaxDevices];
-
-int hip_rc(hipError_t e) { return e == hipSuccess ? NOISE_ERROR_NONE : NOISE_ERROR_SYSTEM; }
-
-/* S-box / T-table are generated on each device once (aesgcm.hip), on a
-   private stream — never the caller's, which may be capturing a graph —
-   and waited for.  Only success is remembered: after a failure the next AES
-   call on that device tries again. */
-hipError_t ensure_aes_tables(hipStream_t)
-{
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
-    if (__atomic_load_n(&g_tab_ready[dev], __ATOMIC_ACQUIRE)) return hipSuccess;
-    std::lock_guard<std::mutex> lk(g_tab_mu[dev]);
-    if (g_tab_ready[dev]) return hipSuccess;
-    hipStream_t s = nullptr;
-    e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(aes_tables_init, dim3(1), dim3(256), 0, s);
-    e = hipGetLastError();
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    (void)hipStreamDestroy(s);
-    if (e == hipSuccess) __atomic_store_n(&g_tab_ready[dev], true, __ATOMIC_RELEASE);
-    return e;
-}
 
 /* Lanes per record for ChaChaPoly: 4 (the fastest split at 64 Ki and 1 Mi
    records, profiles/r01_sweep_*), 8 when the batch is too small to give
@@ -77,77 +41,6 @@ int auto_lanes(uint32_t n_records, uint32_t max_len)
         if (k > need) k = need;
     }
     return k;
-}
-
-template <typename Args>
-using KernelFn = void (*)(Args);
-
-template <typename Args>
-int launch(KernelFn<Args> fn, uint32_t n_records, int lanes, const Args &a, hipStream_t s)
-{
-    if (n_records == 0) return NOISE_ERROR_NONE;
-    const uint64_t threads = (uint64_t)n_records * lanes;
-    const uint32_t blocks = (uint32_t)((threads + 255) / 256);
-    hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, a);
-    return hip_rc(hipGetLastError());
-}
-
-template <int K>
-KernelFn<UniformArgs> chacha_staged_fn(bool open, bool ukey)
-{
-    if (ukey) return open ? chachapoly_open_staged<K, true> : chachapoly_seal_staged<K, true>;
-    return open ? chachapoly_open_staged<K, false> : chachapoly_seal_staged<K, false>;
-}
-
-/* vf: a VERIFY_FIRST open takes the two-pass chachapoly_open_uniform, never
-   the one-pass staged kernel */
-template <bool FAST>
-KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf)
-{
-    switch (k) {
-    case 1: return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
-    case 2: return open ? chachapoly_open_uniform<2, FAST> : chachapoly_seal_uniform<2, FAST>;
-    case 4:
-        if (FAST && !(open && vf)) return chacha_staged_fn<4>(open, ukey);
-        return open ? chachapoly_open_uniform<4, FAST> : chachapoly_seal_uniform<4, FAST>;
-    case 8:
-        if (FAST && !(open && vf)) return chacha_staged_fn<8>(open, ukey);
-        return open ? chachapoly_open_uniform<8, FAST> : chachapoly_seal_uniform<8, FAST>;
-    case 16: return open ? chachapoly_open_uniform<16, FAST> : chachapoly_seal_uniform<16, FAST>;
-    case 32: return open ? chachapoly_open_uniform<32, FAST> : chachapoly_seal_uniform<32, FAST>;
-    case 64: return open ? chachapoly_open_uniform<64, FAST> : chachapoly_seal_uniform<64, FAST>;
-    }
-    return nullptr;
-}
-
-/* ukey: every wave's 64/k records share one state (see u_key_nonce) */
-KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast, bool ukey, bool vf)
-{
-    return fast ? chacha_uniform_fn_t<true>(k, open, ukey, vf)
-                : chacha_uniform_fn_t<false>(k, open, ukey, vf);
-}
-
-/* VF: the FAST opens' two-pass (verify-first) instantiation; the generic
-   layouts' opens are two-pass already */
-template <bool FAST, bool VF>
-KernelFn<RaggedArgs> chacha_ragged_fn_t(int k, bool open)
-{
-    switch (k) {
-    case 1: return open ? chachapoly_open_ragged<1, FAST> : chachapoly_seal_ragged<1, FAST>;
-    case 2: return open ? chachapoly_open_ragged<2, FAST> : chachapoly_seal_ragged<2, FAST>;
-    case 4: return open ? chachapoly_open_ragged<4, FAST, VF> : chachapoly_seal_ragged<4, FAST>;
-    case 8: return open ? chachapoly_open_ragged<8, FAST, VF> : chachapoly_seal_ragged<8, FAST>;
-    case 16: return open ? chachapoly_open_ragged<16, FAST, VF> : chachapoly_seal_ragged<16, FAST>;
-    case 32: return open ? chachapoly_open_ragged<32, FAST, VF> : chachapoly_seal_ragged<32, FAST>;
-    case 64: return open ? chachapoly_open_ragged<64, FAST, VF> : chachapoly_seal_ragged<64, FAST>;
-    }
-    return nullptr;
-}
-
-KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open, bool fast, bool vf)
-{
-    if (!fast) return chacha_ragged_fn_t<false, false>(k, open);
-    return vf ? chacha_ragged_fn_t<true, true>(k, open) : chacha_ragged_fn_t<true, false>(k, open);
 }
 
 /* FAST layout (chachapoly.hip): 16-B aligned record slots whose input may be
@@ -222,55 +115,6 @@ bool ct_ghash(uint32_t flags)
     return (flags & NOISE_AEAD_FLAG_CT_GHASH) || env;
 }
 
-template <bool CT, int WG, int R, int KL = GCM_LANES>
-KernelFn<RaggedArgs> gcm_ragged_pick(bool open, bool fast)
-{
-    return open ? (fast ? gcm_ragged_staged<true, true, WG, CT, R, KL>
-                        : gcm_ragged_staged<true, false, WG, CT, R, KL>)
-                : (fast ? gcm_ragged_staged<false, true, WG, CT, R, KL>
-                        : gcm_ragged_staged<false, false, WG, CT, R, KL>);
-}
-
-/* Ragged AES-GCM launch shape: threads per workgroup, records per group
-   and lanes per record (gcm_ragged_staged).  A workgroup owns its CU (the
-   LDS T-tables), so its time is its longest wave's; pairing a long with a
-   short record per group (R = 2) evens the waves out: +21 % records per
-   CU-second on C5's 64 B-16 KiB mix (profiles/r02/c5_gcm_shape_ab.jsonl).
-   From 131072 records on every CU gets a 512-record window of 4-lane groups;
-   from 65536 on, 256-record windows of 8-lane groups (KL = 8, H^8 Horner)
-   keep all CUs busy with the same pairing (4-lane pairs there would idle
-   half the CUs: 1.55 vs 0.94 ms); smaller batches take 256-thread
-   workgroups over 64-record windows.  NOISE_AEAD_GCM_SHAPE=w1024r1 |
-   w1024r2 | w1024r2k8 forces a shape (A/B runs). */
-struct GcmShape { int wg, r, kl; };
-
-GcmShape gcm_ragged_shape(uint32_t n)
-{
-    static const int forced = [] {
-        const char *e = getenv("NOISE_AEAD_GCM_SHAPE");
-        if (!e) return 0;
-        if (!strcmp(e, "w1024r1")) return 1;
-        if (!strcmp(e, "w1024r2")) return 2;
-        if (!strcmp(e, "w1024r2k8")) return 3;
-        return 0;
-    }();
-    if (forced == 1) return {1024, 1, 4};
-    if (forced == 2) return {1024, 2, 4};
-    if (forced == 3) return {1024, 2, 8};
-    if (n >= 256u * 2 * GCM_WG_RECS) return {1024, 2, 4};
-    if (n >= 256u * GCM_WG_RECS) return {1024, 2, 8};
-    return {256, 1, 4};
-}
-
-template <bool CT>
-KernelFn<RaggedArgs> gcm_ragged_fn(bool open, bool fast, GcmShape sh)
-{
-    if (sh.kl == 8) return gcm_ragged_pick<CT, 1024, 2, 8>(open, fast);
-    if (sh.wg == 1024 && sh.r == 2) return gcm_ragged_pick<CT, 1024, 2>(open, fast);
-    if (sh.wg == 1024) return gcm_ragged_pick<CT, 1024, 1>(open, fast);
-    return gcm_ragged_pick<CT, 256, 1>(open, fast);
-}
-
 int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool open)
 {
     int rc = check_uniform(job, open);
@@ -281,32 +125,20 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
         const bool ukey = k >= 4 && job->recs_per_state % (64u / (uint32_t)k) == 0;
-        KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, uniform_fast(job, open), ukey, a.vf);
-        if (!fn) return NOISE_ERROR_INVALID_PARAM;
         /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC): open
            balances its waves' progress (profiles/r01_prio_ab.jsonl); in the
            seal it measured neutral (profiles/r02/timeline_c2_seal_open_duplex.log) */
         a.balance = open && (uint64_t)job->n_records * (uint32_t)k <= 4096ull * 64;
-        return launch(fn, job->n_records, k, a, s);
+        return chacha_uniform(a, k, open, uniform_fast(job, open), ukey, s);
     }
     if (cipher_id == NOISE_CIPHER_AESGCM) {
         if (job->lanes_per_record && job->lanes_per_record != GCM_LANES)
             return NOISE_ERROR_INVALID_PARAM;
-        rc = hip_rc(ensure_aes_tables(s));
+        rc = hip_rc(ensure_aes_tables());
         if (rc) return rc;
-        const bool ct = ct_ghash(job->flags);
         /* one state per 256-record workgroup + FAST layout -> LDS-staged kernel */
-        if (uniform_fast(job, open) && job->recs_per_state % GCM_WG_RECS == 0) {
-            if (job->n_records == 0) return NOISE_ERROR_NONE;
-            const uint32_t blocks = (job->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
-            hipLaunchKernelGGL(ct ? (open ? gcm_staged<true, true> : gcm_staged<false, true>)
-                                  : (open ? gcm_staged<true, false> : gcm_staged<false, false>),
-                               dim3(blocks), dim3(GCM_WG), 0, s, a);
-            return hip_rc(hipGetLastError());
-        }
-        return launch(ct ? (open ? gcm_uniform<true, true> : gcm_uniform<false, true>)
-                         : (open ? gcm_uniform<true, false> : gcm_uniform<false, false>),
-                      job->n_records, GCM_LANES, a, s);
+        return aes_uniform(a, open, ct_ghash(job->flags),
+                           uniform_fast(job, open) && job->recs_per_state % GCM_WG_RECS == 0, s);
     }
     return NOISE_ERROR_UNKNOWN_ID;
 }
@@ -395,14 +227,7 @@ int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform
         const bool uo = ko >= 4 && oj->recs_per_state % (64u / (uint32_t)ko) == 0;
         if (ks == ko && (ks == 4 || ks == 8) && us == uo && uniform_fast(sj, false) &&
             uniform_fast(oj, true)) {
-            UniformArgs a = to_args(sj), b = to_args(oj);
-            const uint32_t sb = (uint32_t)(((uint64_t)sj->n_records * ks + 255) / 256);
-            const uint32_t ob = (uint32_t)(((uint64_t)oj->n_records * ko + 255) / 256);
-            void (*fn)(UniformArgs, UniformArgs, uint32_t, uint32_t);
-            if (ks == 4) fn = us ? chachapoly_duplex_staged<4, true> : chachapoly_duplex_staged<4, false>;
-            else fn = us ? chachapoly_duplex_staged<8, true> : chachapoly_duplex_staged<8, false>;
-            hipLaunchKernelGGL(fn, dim3(sb + ob), dim3(256), 0, (hipStream_t)stream, a, b, sb, ob);
-            return hip_rc(hipGetLastError());
+            return chacha_duplex(to_args(sj), to_args(oj), ks, us, (hipStream_t)stream);
         }
     }
     if (cipher_id == NOISE_CIPHER_AESGCM && sj->n_records && oj->n_records &&
@@ -411,14 +236,9 @@ int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform
         uniform_fast(sj, false) && uniform_fast(oj, true) &&
         sj->recs_per_state % GCM_WG_RECS == 0 && oj->recs_per_state % GCM_WG_RECS == 0 &&
         ct_ghash(sj->flags) == ct_ghash(oj->flags)) {
-        rc = hip_rc(ensure_aes_tables((hipStream_t)stream));
+        rc = hip_rc(ensure_aes_tables());
         if (rc) return rc;
-        UniformArgs a = to_args(sj), b = to_args(oj);
-        const uint32_t sb = (sj->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
-        const uint32_t ob = (oj->n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
-        hipLaunchKernelGGL(ct_ghash(sj->flags) ? gcm_duplex_staged<true> : gcm_duplex_staged<false>,
-                           dim3(sb + ob), dim3(GCM_WG), 0, (hipStream_t)stream, a, b, sb, ob);
-        return hip_rc(hipGetLastError());
+        return aes_duplex(to_args(sj), to_args(oj), ct_ghash(sj->flags), (hipStream_t)stream);
     }
     rc = run_uniform(cipher_id, sj, stream, false);
     if (!rc) rc = run_uniform(cipher_id, oj, stream, true);
@@ -445,35 +265,15 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
            lengths (C5's ChaCha kernels -2.5 % seal / -4 % open at 64 Ki
            records vs 4 lanes, profiles/r02/c5_lanes_ab.jsonl) */
         if (!job->lanes_per_record && k == 4 && job->n_records < 2u * 65536u) k = 8;
-        KernelFn<RaggedArgs> fn =
-            chacha_ragged_fn(k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0, a.vf != 0);
-        if (!fn) return NOISE_ERROR_INVALID_PARAM;
-        return launch(fn, job->n_records, k, a, s);
+        return chacha_ragged(a, k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0, s);
     }
     if (cipher_id == NOISE_CIPHER_AESGCM) {
-        int rc = hip_rc(ensure_aes_tables(s));
+        int rc = hip_rc(ensure_aes_tables());
         if (rc) return rc;
-        if (job->n_records == 0) return NOISE_ERROR_NONE;
-        const bool ct = ct_ghash(job->flags);
-        /* LDS-staged kernel: 1024-thread workgroups over 256-record windows;
-           a batch too small to give every CU one of those uses 256-thread
-           workgroups over 64-record windows instead (4x the workgroups) */
-        if (job->lanes_per_record == 0 && job->n_records <= WIDE_MAX_RECORDS) {
-            /* small batch: a workgroup per record (latency, not throughput);
-               lanes_per_record = 4 keeps the windowed 4-lane kernels */
-            hipLaunchKernelGGL(ct ? (open ? gcm_wide<true, true> : gcm_wide<false, true>)
-                                  : (open ? gcm_wide<true, false> : gcm_wide<false, false>),
-                               dim3(job->n_records), dim3(256), 0, s, a);
-            return hip_rc(hipGetLastError());
-        }
-        const bool fast = (job->flags & NOISE_AEAD_FLAG_FAST) != 0;
-        const GcmShape sh = gcm_ragged_shape(job->n_records);
-        const uint32_t per = (uint32_t)(sh.wg / sh.kl * sh.r); /* records per window */
-        const uint32_t blocks = (job->n_records + per - 1) / per;
-        KernelFn<RaggedArgs> fn = ct ? gcm_ragged_fn<true>(open, fast, sh)
-                                     : gcm_ragged_fn<false>(open, fast, sh);
-        hipLaunchKernelGGL(fn, dim3(blocks), dim3(sh.wg), 0, s, a);
-        return hip_rc(hipGetLastError());
+        /* small batch with automatic lanes: a workgroup per record (latency);
+           lanes_per_record = 4 keeps the windowed 4-lane kernels */
+        return aes_ragged(a, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0, ct_ghash(job->flags),
+                          job->lanes_per_record == 0 && job->n_records <= WIDE_MAX_RECORDS, s);
     }
     return NOISE_ERROR_UNKNOWN_ID;
 }
@@ -520,11 +320,9 @@ int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_
         return hip_rc(hipMemcpyAsync(d_ctx, d_raw_keys, (size_t)n_states * 32,
                                      hipMemcpyDeviceToDevice, s));
     if (cipher_id == NOISE_CIPHER_AESGCM) {
-        int rc = hip_rc(ensure_aes_tables(s));
+        int rc = hip_rc(ensure_aes_tables());
         if (rc) return rc;
-        hipLaunchKernelGGL(gcm_prepare, dim3(n_states), dim3(256), 0, s, d_raw_keys,
-                           (AesCtx *)d_ctx, n_states);
-        return hip_rc(hipGetLastError());
+        return aes_prepare(d_raw_keys, n_states, d_ctx, s);
     }
     return NOISE_ERROR_UNKNOWN_ID;
 }

@@ -120,6 +120,8 @@ __device__ __forceinline__ uint32_t snake_rank(uint32_t g, int p)
 
 /* AES-GCM per-state device context (prepared once per key). */
 constexpr int GCM_LANES = 4;                    /* lanes per record */
+constexpr int GCM_WG = 1024;                    /* threads per staged workgroup */
+constexpr int GCM_WG_RECS = GCM_WG / GCM_LANES; /* records per staged workgroup */
 constexpr int GHASH_TAB_ENTRIES = 32 * 16;      /* 4-bit positional table */
 struct AesCtx {
     uint32_t rk[60];                            /* AES-256 round keys, BE words */

@@ -518,8 +518,6 @@ __global__ __launch_bounds__(256) void gcm_ragged(RaggedArgs a)
  *    x 16 B per nibble position: a 16-lane b128 group is conflict-free).
  * The per-block work then touches no global memory but the record bytes.
  */
-constexpr int GCM_WG = 1024;                  /* threads per staged workgroup */
-constexpr int GCM_WG_RECS = GCM_WG / GCM_LANES;
 
 struct GcmLds {
     uint32_t te[2][256][64]; /* [Te0|Te1 or Te2|Te3][row][32 + 32 copies] */

@@ -1392,7 +1392,7 @@ __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
         ok = open_any<K, FAST>(rv, k);
     }
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
-    if (!ok && !VF) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)k, K);
+    if (!ok && !a.vf) scrub_rejected(rv.dst, rv.src, rv.len, (uint32_t)k, K);
 }
 
 } // namespace na

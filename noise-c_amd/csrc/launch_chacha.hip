@@ -1,0 +1,112 @@
+/*
+ * launch_chacha.hip — launchers of the ChaChaPoly kernels (chachapoly.hip):
+ * picks the instantiation for the lane count, layout, key sharing and open
+ * order of a job and launches it.  Called by the C-ABI layer (aead_api.hip)
+ * through launch.h.
+ */
+#include "launch.h"
+#include "chachapoly.hip"
+
+namespace na {
+namespace {
+
+template <typename Args>
+using KernelFn = void (*)(Args);
+
+template <typename Args>
+int launch(KernelFn<Args> fn, uint32_t n_records, int lanes, const Args &a, hipStream_t s)
+{
+    if (n_records == 0) return NOISE_ERROR_NONE;
+    const uint64_t threads = (uint64_t)n_records * lanes;
+    const uint32_t blocks = (uint32_t)((threads + 255) / 256);
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, a);
+    return hip_rc(hipGetLastError());
+}
+
+template <int K>
+KernelFn<UniformArgs> chacha_staged_fn(bool open, bool ukey)
+{
+    if (ukey) return open ? chachapoly_open_staged<K, true> : chachapoly_seal_staged<K, true>;
+    return open ? chachapoly_open_staged<K, false> : chachapoly_seal_staged<K, false>;
+}
+
+/* vf: a VERIFY_FIRST open takes the two-pass chachapoly_open_uniform, never
+   the one-pass staged kernel */
+template <bool FAST>
+KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf)
+{
+    switch (k) {
+    case 1: return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
+    case 2: return open ? chachapoly_open_uniform<2, FAST> : chachapoly_seal_uniform<2, FAST>;
+    case 4:
+        if (FAST && !(open && vf)) return chacha_staged_fn<4>(open, ukey);
+        return open ? chachapoly_open_uniform<4, FAST> : chachapoly_seal_uniform<4, FAST>;
+    case 8:
+        if (FAST && !(open && vf)) return chacha_staged_fn<8>(open, ukey);
+        return open ? chachapoly_open_uniform<8, FAST> : chachapoly_seal_uniform<8, FAST>;
+    case 16: return open ? chachapoly_open_uniform<16, FAST> : chachapoly_seal_uniform<16, FAST>;
+    case 32: return open ? chachapoly_open_uniform<32, FAST> : chachapoly_seal_uniform<32, FAST>;
+    case 64: return open ? chachapoly_open_uniform<64, FAST> : chachapoly_seal_uniform<64, FAST>;
+    }
+    return nullptr;
+}
+
+/* ukey: every wave's 64/k records share one state (see u_key_nonce) */
+KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast, bool ukey, bool vf)
+{
+    return fast ? chacha_uniform_fn_t<true>(k, open, ukey, vf)
+                : chacha_uniform_fn_t<false>(k, open, ukey, vf);
+}
+
+/* VF: the FAST opens' two-pass (verify-first) instantiation; the generic
+   layouts' opens are two-pass already */
+template <bool FAST, bool VF>
+KernelFn<RaggedArgs> chacha_ragged_fn_t(int k, bool open)
+{
+    switch (k) {
+    case 1: return open ? chachapoly_open_ragged<1, FAST> : chachapoly_seal_ragged<1, FAST>;
+    case 2: return open ? chachapoly_open_ragged<2, FAST> : chachapoly_seal_ragged<2, FAST>;
+    case 4: return open ? chachapoly_open_ragged<4, FAST, VF> : chachapoly_seal_ragged<4, FAST>;
+    case 8: return open ? chachapoly_open_ragged<8, FAST, VF> : chachapoly_seal_ragged<8, FAST>;
+    case 16: return open ? chachapoly_open_ragged<16, FAST, VF> : chachapoly_seal_ragged<16, FAST>;
+    case 32: return open ? chachapoly_open_ragged<32, FAST, VF> : chachapoly_seal_ragged<32, FAST>;
+    case 64: return open ? chachapoly_open_ragged<64, FAST, VF> : chachapoly_seal_ragged<64, FAST>;
+    }
+    return nullptr;
+}
+
+KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open, bool fast, bool vf)
+{
+    if (!fast) return chacha_ragged_fn_t<false, false>(k, open);
+    return vf ? chacha_ragged_fn_t<true, true>(k, open) : chacha_ragged_fn_t<true, false>(k, open);
+}
+
+} // namespace
+
+int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, bool ukey, hipStream_t s)
+{
+    KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, fast, ukey, a.vf != 0);
+    if (!fn) return NOISE_ERROR_INVALID_PARAM;
+    return launch(fn, a.n_records, k, a, s);
+}
+
+int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, hipStream_t s)
+{
+    const uint32_t sb = (uint32_t)(((uint64_t)a.n_records * k + 255) / 256);
+    const uint32_t ob = (uint32_t)(((uint64_t)b.n_records * k + 255) / 256);
+    void (*fn)(UniformArgs, UniformArgs, uint32_t, uint32_t);
+    if (k == 4) fn = ukey ? chachapoly_duplex_staged<4, true> : chachapoly_duplex_staged<4, false>;
+    else if (k == 8) fn = ukey ? chachapoly_duplex_staged<8, true> : chachapoly_duplex_staged<8, false>;
+    else return NOISE_ERROR_INVALID_PARAM;
+    hipLaunchKernelGGL(fn, dim3(sb + ob), dim3(256), 0, s, a, b, sb, ob);
+    return hip_rc(hipGetLastError());
+}
+
+int chacha_ragged(const RaggedArgs &a, int k, bool open, bool fast, hipStream_t s)
+{
+    KernelFn<RaggedArgs> fn = chacha_ragged_fn(k, open, fast, a.vf != 0);
+    if (!fn) return NOISE_ERROR_INVALID_PARAM;
+    return launch(fn, a.n_records, k, a, s);
+}
+
+} // namespace na
