@@ -381,6 +381,10 @@ int noise_strerror(int err, char *buf, size_t size);
  *   the allocation; this returns it (and its size) so a test can read back
  *   zeros.  Leaks by design; never set it in production. */
 void noise_aead_debug_batch_stats(uint64_t *rounds, uint64_t *dispatched);
+/* noise_aead_debug_worker_stamps: the phase times (10-ns ticks) of the
+ *   resident single-record worker's last request on the current device:
+ *   fence, inputs in LDS, computed, results written, released (n <= 5). */
+void noise_aead_debug_worker_stamps(uint32_t *out, int n);
 void *noise_aead_debug_last_freed_ctx(size_t *bytes);
 
 /* Default lanes per record the library picks for a batch of n records. */

@@ -89,3 +89,19 @@ uint32_t na_aes_lanes(uint32_t n_records)
     (void)n_records;
     return 0;
 }
+
+/* the resident worker is GPU-only: the host paths take the launch path */
+int na_worker_enabled(void) { return 0; }
+
+int na_worker_crypt(int cipher_id, const uint8_t *key, const void *h_ctx, uint32_t gen, uint64_t nonce,
+                    const uint8_t *ad, size_t ad_len, uint8_t *data, size_t len, int open)
+{
+    (void)cipher_id; (void)key; (void)h_ctx; (void)gen; (void)nonce; (void)ad; (void)ad_len;
+    (void)data; (void)len; (void)open;
+    return NOISE_ERROR_NOT_APPLICABLE;
+}
+
+void noise_aead_debug_worker_stamps(uint32_t *out, int n)
+{
+    for (int i = 0; i < n; ++i) out[i] = 0;
+}

@@ -26,9 +26,10 @@
 
 namespace na {
 
-__device__ uint32_t g_te0[256]; /* T-table: BE word (2s, s, s, 3s) */
-__device__ uint32_t g_sbox[256];
-__device__ int g_tables_ready;
+/* per translation unit (static): launch_aes.hip's kernels read these; the
+   resident worker (worker.hip) builds its own copy in LDS */
+static __device__ uint32_t g_te0[256]; /* T-table: BE word (2s, s, s, 3s) */
+static __device__ uint32_t g_sbox[256];
 
 NA_DEV uint32_t xtime8(uint32_t a) { return ((a << 1) ^ ((a & 0x80) ? 0x1b : 0)) & 0xff; }
 
@@ -43,10 +44,9 @@ NA_DEV uint32_t gf8_mul(uint32_t a, uint32_t b)
     return p;
 }
 
-/* FIPS-197 S-box and T-table, generated on the device (inverse = x^254). */
-__global__ void aes_tables_init()
+/* FIPS-197 S-box entry x and T-table entry (inverse = x^254). */
+NA_DEV void aes_table_entry(uint32_t x, uint32_t &sbox, uint32_t &te0)
 {
-    const uint32_t x = threadIdx.x;
     uint32_t inv = 1, base = x;
     for (int e = 254; e; e >>= 1) {
         if (e & 1) inv = gf8_mul(inv, base);
@@ -56,11 +56,19 @@ __global__ void aes_tables_init()
     uint32_t s = inv;
     for (int i = 1; i <= 4; ++i) s ^= ((inv << i) | (inv >> (8 - i))) & 0xff;
     s ^= 0x63;
-    g_sbox[x] = s;
+    sbox = s;
     const uint32_t s2 = xtime8(s), s3 = s2 ^ s;
-    g_te0[x] = (s2 << 24) | (s << 16) | (s << 8) | s3;
-    if (x == 0) g_tables_ready = 1;
+    te0 = (s2 << 24) | (s << 16) | (s << 8) | s3;
 }
+
+#ifndef NA_NO_SETUP_KERNELS /* worker.hip includes only the device functions */
+/* The tables, generated on the device once (launch_aes.hip ensure_aes_tables). */
+__global__ void aes_tables_init()
+{
+    const uint32_t x = threadIdx.x;
+    aes_table_entry(x, g_sbox[x], g_te0[x]);
+}
+#endif
 
 NA_DEV uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 
@@ -274,6 +282,7 @@ NA_DEV void gf_mul_bytes(const uint8_t x[16], const uint8_t h[16], uint8_t out[1
     for (int j = 0; j < 16; ++j) out[j] = z[j];
 }
 
+#ifndef NA_NO_SETUP_KERNELS
 /* One workgroup per state: round keys, H, and the H^1..H^4 tables. */
 __global__ __launch_bounds__(256) void gcm_prepare(const uint8_t *__restrict__ raw_keys,
                                                    AesCtx *__restrict__ ctx, uint32_t n_states)
@@ -350,6 +359,7 @@ __global__ __launch_bounds__(256) void gcm_prepare(const uint8_t *__restrict__ r
                      ((uint32_t)acc[4 * w + 2] << 16) | ((uint32_t)acc[4 * w + 3] << 24);
     }
 }
+#endif
 
 /* ---------------------------------------------------------------- records */
 
@@ -1075,36 +1085,25 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
  * CTR, then GHASH over the CT just written.  Open: GHASH and tag check
  * first, CTR only when the tag verified (cipher-aesgcm.c:184-186).
  */
+/* One record on a 256-thread workgroup (the whole workgroup calls it):
+   te/sb/h4 are the LDS tables (h4: the record's H^4 multiply table when not
+   CT), verdict an LDS word.  Returns (open) whether the tag verified; writes
+   status when given; a rejected record's output is left alone here (the
+   caller scrubs).  Shared by gcm_wide and the resident worker (worker.hip). */
 template <bool OPEN, bool CT>
-__global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
+NA_DEV bool gcm_wide_record(const uint8_t *src, uint8_t *dst, const uint8_t *ad, uint32_t ad_len,
+                            uint32_t len, uint64_t nonce, const AesCtx *ctx, const uint32_t *te,
+                            const uint32_t *sb, const uint4 *h4, uint32_t *verdict, uint8_t *status)
 {
     constexpr int K = GCM_LANES;
-    __shared__ uint32_t te[256], sb[256];
-    __shared__ uint4 h4[GHASH_TAB_ENTRIES];
-    __shared__ uint32_t verdict;
-    const uint32_t rec = blockIdx.x, t = threadIdx.x;
-    const RecDesc d = a.recs[rec];
-    if (reject_len(a, rec, d.len, t == 0)) return; /* uniform over the workgroup */
-    const AesCtx *ctx = (const AesCtx *)(a.keys + d.ctx_off);
-    const uint8_t *src = a.in + d.in_off;
-    uint8_t *dst = a.out + d.out_off;
-    const uint32_t len = d.len, M = (len + 15) / 16;
-    for (uint32_t i = t; i < 256; i += 256) {
-        te[i] = g_te0[i];
-        sb[i] = g_sbox[i];
-    }
-    if (!CT)
-        for (uint32_t i = t; i < (uint32_t)GHASH_TAB_ENTRIES; i += 256)
-            h4[i] = ((const uint4 *)ctx->tab[K - 1])[i];
-    __syncthreads();
+    const uint32_t t = threadIdx.x, M = (len + 15) / 16;
     const uint32_t *rk = ctx->rk;
-
     if (!OPEN) {
         for (uint32_t b = t; b < M; b += 256) {
             const uint32_t nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
             uint32_t x[4], ks[4];
             load16(src + 16 * b, nb, x);
-            aes_ctr_block(rk, te, sb, d.nonce, 2 + b, ks);
+            aes_ctr_block(rk, te, sb, nonce, 2 + b, ks);
 #pragma unroll
             for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
             store16(dst + 16 * b, nb, x);
@@ -1114,7 +1113,7 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
     if (t < (uint32_t)K) {
         const int l = (int)t;
         const uint8_t *ct = OPEN ? src : dst;
-        const uint32_t A = (d.ad_len + 15) / 16, n = A + M + 1;
+        const uint32_t A = (ad_len + 15) / 16, n = A + M + 1;
         const uint32_t c0 = ((uint32_t)l + n) % K;
         uint32_t h4n[4] = {0, 0, 0, 0};
         if constexpr (CT) {
@@ -1126,13 +1125,13 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
             if (i != c0) gh_step<CT>(acc, h4, h4n);
             uint32_t x[4];
             if (i < A) {
-                const uint32_t rem = d.ad_len - 16 * i;
-                load16(a.ad + d.ad_off + 16 * i, rem >= 16 ? 16u : rem, x);
+                const uint32_t rem = ad_len - 16 * i;
+                load16(ad + 16 * i, rem >= 16 ? 16u : rem, x);
             } else if (i < A + M) {
                 const uint32_t b = i - A, rem = len - 16 * b;
                 load16(ct + 16 * b, rem >= 16 ? 16u : rem, x);
             } else {
-                const uint64_t ab = (uint64_t)d.ad_len * 8, cb = (uint64_t)len * 8;
+                const uint64_t ab = (uint64_t)ad_len * 8, cb = (uint64_t)len * 8;
                 x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
                 x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
             }
@@ -1146,36 +1145,59 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
             for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
         if constexpr (CT) gh_to_nat(acc);
         uint32_t ej[4];
-        aes_ctr_block(rk, te, sb, d.nonce, 1u, ej);
+        aes_ctr_block(rk, te, sb, nonce, 1u, ej);
         const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
         if (!OPEN) {
             if (l == K - 1) store16(dst + len, 16, tag);
-            if (l == K - 1 && a.status) a.status[rec] = 0;
+            if (l == K - 1 && status) *status = 0;
         } else if (l == 0) {
             uint32_t got[4];
             load16(src + len, 16, got);
             const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) |
                              (tag[3] ^ got[3])) == 0;
-            verdict = ok;
-            if (a.status) a.status[rec] = ok ? 0 : 1;
+            *verdict = ok;
+            if (status) *status = ok ? 0 : 1;
         }
     }
-    if (OPEN) {
-        __syncthreads();
-        if (!verdict) { /* nothing decrypted */
-            if (!a.vf) scrub_rejected(dst, src, len, t, 256);
-            return;
-        }
-        for (uint32_t b = t; b < M; b += 256) {
-            const uint32_t nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
-            uint32_t x[4], ks[4];
-            load16(src + 16 * b, nb, x);
-            aes_ctr_block(rk, te, sb, d.nonce, 2 + b, ks);
+    if (!OPEN) return true;
+    __syncthreads();
+    if (!*verdict) return false; /* nothing decrypted */
+    for (uint32_t b = t; b < M; b += 256) {
+        const uint32_t nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
+        uint32_t x[4], ks[4];
+        load16(src + 16 * b, nb, x);
+        aes_ctr_block(rk, te, sb, nonce, 2 + b, ks);
 #pragma unroll
-            for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
-            store16(dst + 16 * b, nb, x);
-        }
+        for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+        store16(dst + 16 * b, nb, x);
     }
+    return true;
+}
+
+template <bool OPEN, bool CT>
+__global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
+{
+    constexpr int K = GCM_LANES;
+    __shared__ uint32_t te[256], sb[256];
+    __shared__ uint4 h4[GHASH_TAB_ENTRIES];
+    __shared__ uint32_t verdict;
+    const uint32_t rec = blockIdx.x, t = threadIdx.x;
+    const RecDesc d = a.recs[rec];
+    if (reject_len(a, rec, d.len, t == 0)) return; /* uniform over the workgroup */
+    const AesCtx *ctx = (const AesCtx *)(a.keys + d.ctx_off);
+    const uint8_t *src = a.in + d.in_off;
+    uint8_t *dst = a.out + d.out_off;
+    for (uint32_t i = t; i < 256; i += 256) {
+        te[i] = g_te0[i];
+        sb[i] = g_sbox[i];
+    }
+    if (!CT)
+        for (uint32_t i = t; i < (uint32_t)GHASH_TAB_ENTRIES; i += 256)
+            h4[i] = ((const uint4 *)ctx->tab[K - 1])[i];
+    __syncthreads();
+    const bool ok = gcm_wide_record<OPEN, CT>(src, dst, a.ad + d.ad_off, d.ad_len, d.len, d.nonce, ctx,
+                                              te, sb, h4, &verdict, a.status ? a.status + rec : nullptr);
+    if (OPEN && !ok && !a.vf) scrub_rejected(dst, src, d.len, t, 256);
 }
 
 } // namespace na

@@ -859,11 +859,12 @@ NA_DEV void u_key_nonce(const UniformArgs &a, uint32_t rec0, uint32_t rc, uint32
     n_hi = (uint32_t)(n >> 32);
 }
 
+/* wave_job: the wave's 64/K consecutive records start at wave_job * (64/K) */
 template <int K, bool UKEY>
-NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uint32_t blk)
+NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uint32_t wave_job)
 {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t rec0 = ((blk * 256u + threadIdx.x) >> 6) * (64 / K);
+    const uint32_t rec0 = wave_job * (64 / K);
     const uint32_t rec_raw = rec0 + lane / K;
     const bool live = rec_raw < a.n_records;
     const uint32_t rc = live ? rec_raw : a.n_records - 1;
@@ -940,10 +941,10 @@ NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
    (cipher-chachapoly.c:140-150) — and out of place it zeroes the record's
    output (scrub_rejected's contract). */
 template <int K, bool UKEY>
-NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uint32_t blk)
+NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uint32_t wave_job)
 {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t rec0 = ((blk * 256u + threadIdx.x) >> 6) * (64 / K);
+    const uint32_t rec0 = wave_job * (64 / K);
     const uint32_t rec_raw = rec0 + lane / K;
     const bool live = rec_raw < a.n_records;
     const uint32_t rc = live ? rec_raw : a.n_records - 1;
@@ -1280,13 +1281,16 @@ NA_DEV RecView ragged_view(const RaggedArgs &a, uint32_t rec)
     return rv;
 }
 
+/* the grid-wide wave index of this thread's wave in workgroup b */
+NA_DEV uint32_t wave_of(uint32_t b) { return (b * 256u + threadIdx.x) >> 6; }
+
 /* LDS-staged uniform FAST batches, K = 4 or 8 lanes per record */
 template <int K, bool UKEY>
 __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_seal_staged(UniformArgs a)
 {
     __shared__ uint4 tiles[4][512]; /* two 4 KB tiles per wave */
     __shared__ FinSlot fin[4];
-    seal_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], blockIdx.x);
+    seal_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], wave_of(blockIdx.x));
 }
 
 template <int K, bool UKEY>
@@ -1294,7 +1298,7 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_open_staged(Uni
 {
     __shared__ uint4 tiles[4][512];
     __shared__ FinSlot fin[4];
-    open_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], blockIdx.x);
+    open_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], wave_of(blockIdx.x));
 }
 
 /* Duplex: one launch over two independent uniform jobs — seal job `s` and
@@ -1321,8 +1325,56 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_staged(
         open = o_blocks > s_blocks;
         b -= n;
     }
-    if (open) open_il_staged<K, UKEY>(o, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], b);
-    else seal_il_staged<K, UKEY>(s, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], b);
+    if (open) open_il_staged<K, UKEY>(o, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], wave_of(b));
+    else seal_il_staged<K, UKEY>(s, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], wave_of(b));
+}
+
+/* Persistent duplex: the same two jobs as chachapoly_duplex_staged, but a grid
+   of at most the resident workgroups (4 per CU) whose waves take wave-jobs
+   (64/K records of one job) from a ticket counter until none are left:
+   tickets alternate seal / open while both jobs have some, then the longer
+   job's remainder.  A wave goes on to its next wave-job as soon as it
+   finishes one — no workgroup waits for its slowest wave and no second
+   generation is dispatched — and a faster SIMD simply takes more wave-jobs,
+   so every SIMD keeps four waves until the tickets run out.  Each wave-job
+   runs exactly the code of the separate kernels, so results are identical.
+   ctr[0] hands out tickets, ctr[1] counts finished waves; the last wave to
+   finish resets both, so the next launch on the stream starts from zero
+   (stream order; the library keeps one counter pair per stream). */
+template <int K, bool UKEY>
+__global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_persist(
+    UniformArgs s, UniformArgs o, uint32_t s_jobs, uint32_t o_jobs, uint32_t *ctr)
+{
+    __shared__ uint4 tiles[4][512];
+    __shared__ FinSlot fin[4];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t n = min(s_jobs, o_jobs), total = s_jobs + o_jobs;
+    for (;;) {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(&ctr[0], 1u);
+        t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)t, 0, 64));
+        if (t >= total) break; /* every wave draws exactly one ticket past the end */
+        bool open;
+        uint32_t j;
+        if (t < 2 * n) {
+            open = t & 1;
+            j = t >> 1;
+        } else {
+            open = o_jobs > s_jobs;
+            j = t - n;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (open) open_il_staged<K, UKEY>(o, tiles[w], &fin[w], j);
+        else seal_il_staged<K, UKEY>(s, tiles[w], &fin[w], j);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) {
+        const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+        if (atomicAdd(&ctr[1], 1u) == waves - 1) { /* every wave has drawn its last ticket */
+            atomicExch(&ctr[0], 0u);
+            atomicExch(&ctr[1], 0u);
+        }
+    }
 }
 
 template <int K, bool FAST>

@@ -147,6 +147,12 @@ void *noise_aead_debug_last_freed_ctx(size_t *bytes)
 
 static void release_ctx(HipCipherState *st)
 {
+    if (st->h_ctx) { /* the worker's pinned copy holds key material too */
+        na_clean(st->h_ctx, noise_aead_dev_ctx_bytes(st->parent.cipher_id));
+        (void)hipHostFree(st->h_ctx);
+        st->h_ctx = NULL;
+        st->h_ctx_ready = 0;
+    }
     if (!st->d_ctx) return;
     const size_t bytes = noise_aead_dev_ctx_bytes(st->parent.cipher_id);
     scrub_device(st->d_ctx, bytes, st->device); /* the context holds key material */
@@ -537,11 +543,47 @@ static void hip_init_key(NoiseCipherState *state, const uint8_t *key)
     HipCipherState *st = (HipCipherState *)state;
     memcpy(st->key, key, 32);
     st->ctx_ready = 0;
+    st->h_ctx_ready = 0;
+}
+
+/* A single record through the resident worker (worker.hip): no kernel launch
+   per call.  ChaChaPoly passes the key itself; AES-GCM a pinned host copy of
+   the state's device context, made once per key.  NOISE_ERROR_NOT_APPLICABLE:
+   take the launch path. */
+static int worker_crypt(HipCipherState *st, const uint8_t *ad, size_t ad_len, uint8_t *data,
+                        size_t len, int open)
+{
+    if (!na_worker_enabled()) return NOISE_ERROR_NOT_APPLICABLE;
+    const void *h = NULL;
+    if (st->parent.cipher_id == NOISE_CIPHER_AESGCM) {
+        if (!st->h_ctx_ready) {
+            const size_t bytes = noise_aead_dev_ctx_bytes(NOISE_CIPHER_AESGCM);
+            Staging *sg = na_stage_get(64);
+            if (!sg || na_ensure_ctx(st, sg)) return NOISE_ERROR_NOT_APPLICABLE;
+            if (!st->h_ctx && hipHostMalloc((void **)&st->h_ctx, bytes,
+                                            hipHostMallocMapped | hipHostMallocCoherent |
+                                            hipHostMallocPortable) != hipSuccess) {
+                st->h_ctx = NULL;
+                return NOISE_ERROR_NOT_APPLICABLE;
+            }
+            if (hipMemcpy(st->h_ctx, st->d_ctx, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+                return NOISE_ERROR_NOT_APPLICABLE;
+            /* a new generation: the worker's cached copy of this address is stale */
+            static uint32_t gen_counter;
+            st->h_ctx_gen = __atomic_add_fetch(&gen_counter, 1, __ATOMIC_RELAXED);
+            st->h_ctx_ready = 1;
+        }
+        h = st->h_ctx;
+    }
+    return na_worker_crypt(st->parent.cipher_id, st->key, h, st->h_ctx_gen, st->parent.n, ad, ad_len,
+                           data, len, open);
 }
 
 static int hip_crypt(NoiseCipherState *state, const uint8_t *ad, size_t ad_len,
                      uint8_t *data, size_t len, int open)
 {
+    const int wrc = worker_crypt((HipCipherState *)state, ad, ad_len, data, len, open);
+    if (wrc != NOISE_ERROR_NOT_APPLICABLE) return wrc;
     Job j;
     j.st = (HipCipherState *)state;
     j.ad = ad;

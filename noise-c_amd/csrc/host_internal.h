@@ -54,6 +54,10 @@ typedef struct {
     uint64_t b_upd;    /* round whose outcome last set b_window / b_forge */
     uint64_t b_window; /* records dispatched per round (0 = all) */
     uint64_t b_sent;   /* records dispatched in the current round */
+    /* AES-GCM: pinned host copy of d_ctx for the resident worker (worker.hip) */
+    uint8_t *h_ctx;
+    int h_ctx_ready;
+    uint32_t h_ctx_gen;  /* generation the copy was written at */
 } HipCipherState;
 
 #define MAX_CHUNKS 64
@@ -72,6 +76,13 @@ typedef struct {
     uint8_t *d;        /* device */
     size_t cap;
 } Staging;
+
+/* The resident single-record worker (worker.hip): na_worker_crypt returns
+   NOISE_ERROR_NOT_APPLICABLE when the record must take the launch path. */
+NA_HIDDEN int na_worker_enabled(void);
+NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, const void *h_ctx, uint32_t gen,
+                              uint64_t nonce, const uint8_t *ad, size_t ad_len, uint8_t *data,
+                              size_t len, int open);
 
 NA_HIDDEN Staging *na_stage_get(size_t bytes);
 NA_HIDDEN int na_ensure_ctx(HipCipherState *st, Staging *sg);

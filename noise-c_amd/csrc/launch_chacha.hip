@@ -6,6 +6,10 @@
  */
 #include "launch.h"
 #include "chachapoly.hip"
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
 
 namespace na {
 namespace {
@@ -81,6 +85,65 @@ KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open, bool fast, bool vf)
     return vf ? chacha_ragged_fn_t<true, true>(k, open) : chacha_ragged_fn_t<true, false>(k, open);
 }
 
+/* The ticket counter pair of chachapoly_duplex_persist for (device, stream):
+   zeroed once, stream-ordered before the first launch; each launch leaves it
+   zeroed for the next one on the same stream. */
+std::mutex g_ctr_mu;
+std::map<std::pair<int, hipStream_t>, uint32_t *> g_ctr;
+
+uint32_t *ticket_counter(hipStream_t s)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ctr_mu);
+    uint32_t *&c = g_ctr[{dev, s}];
+    if (!c) {
+        if (hipMalloc((void **)&c, 64) != hipSuccess) {
+            c = nullptr;
+            return nullptr;
+        }
+        if (hipMemsetAsync(c, 0, 64, s) != hipSuccess) return nullptr;
+    }
+    return c;
+}
+
+/* Resident workgroups of a kernel on this device (CUs x occupancy). */
+template <typename F>
+uint32_t resident_blocks(F fn)
+{
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || per < 1)
+        return 0;
+    return (uint32_t)(cus * per);
+}
+
+/* NOISE_AEAD_DUPLEX=persist | plain selects the duplex kernel (A/B runs). */
+bool duplex_persist()
+{
+    static const int v = [] {
+        const char *e = getenv("NOISE_AEAD_DUPLEX");
+        return e && !strcmp(e, "persist") ? 1 : 0;
+    }();
+    return v != 0;
+}
+
+template <int K, bool UKEY>
+int duplex_persist_launch(const UniformArgs &a, const UniformArgs &b, hipStream_t s)
+{
+    auto fn = chachapoly_duplex_persist<K, UKEY>;
+    static uint32_t resident = 0; /* one device model per process: MI355X */
+    if (!resident) resident = resident_blocks(fn);
+    uint32_t *ctr = ticket_counter(s);
+    if (!resident || !ctr) return NOISE_ERROR_SYSTEM;
+    const uint32_t sj = (uint32_t)(((uint64_t)a.n_records * K + 63) / 64);
+    const uint32_t oj = (uint32_t)(((uint64_t)b.n_records * K + 63) / 64);
+    const uint32_t want = (sj + oj + 3) / 4;
+    hipLaunchKernelGGL(fn, dim3(want < resident ? want : resident), dim3(256), 0, s, a, b, sj, oj, ctr);
+    return hip_rc(hipGetLastError());
+}
+
 } // namespace
 
 int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, bool ukey, hipStream_t s)
@@ -92,6 +155,11 @@ int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, bool ukey,
 
 int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, hipStream_t s)
 {
+    if (duplex_persist()) {
+        if (k == 4) return ukey ? duplex_persist_launch<4, true>(a, b, s) : duplex_persist_launch<4, false>(a, b, s);
+        if (k == 8) return ukey ? duplex_persist_launch<8, true>(a, b, s) : duplex_persist_launch<8, false>(a, b, s);
+        return NOISE_ERROR_INVALID_PARAM;
+    }
     const uint32_t sb = (uint32_t)(((uint64_t)a.n_records * k + 255) / 256);
     const uint32_t ob = (uint32_t)(((uint64_t)b.n_records * k + 255) / 256);
     void (*fn)(UniformArgs, UniformArgs, uint32_t, uint32_t);

@@ -1,0 +1,452 @@
+/*
+ * worker.hip — the resident single-record engine of the CipherState calls.
+ *
+ * A per-record noise_cipherstate_encrypt/decrypt (src/protocol/cipherstate.c
+ * :293-410, the call pattern of examples/echo) is one record of 1 B - 64 KiB.
+ * Launching a kernel and waiting for it costs ~20 us on its own, 5x the
+ * reference's whole ~4 us CPU call.  Instead, the first call on a device
+ * starts ONE resident workgroup (256 threads) on a private stream; it polls
+ * a request slot in pinned, fine-grained host memory and serves records as
+ * they are posted:
+ *
+ *   host                                    worker (aead_worker)
+ *   write AD || record || tag to data[]
+ *   write op, cipher, ctx, nonce, lengths
+ *   seq = k        (release, system)  --->  sees seq != last (acquire, system)
+ *                                           copies AD || record into LDS,
+ *                                           runs the record (the same device
+ *                                           code as the ragged kernels),
+ *                                           writes it back, fences,
+ *   spins until done == k       <------     done = k (release, system)
+ *   reads status, copies out
+ *
+ * The worker exits on its own after IDLE of no requests (and after at most
+ * LIFETIME), or when the host sets stop; every exit path is reached by every
+ * thread of the workgroup (one barrier-synchronised loop).  Before leaving it
+ * sets `exiting` and looks at seq once more, so a request posted meanwhile
+ * is either served or seen by the host (exiting set, done behind): the host
+ * then waits for the stream and starts a new worker at the same seq.  At most
+ * one worker per device is alive; calls on it are serialised by a mutex.
+ *
+ * Key material reaches the worker through the slot as well: the ChaCha key
+ * itself, or for AES-GCM a pinned host copy of the state's device context
+ * (made once per key).  A resident kernel never reads device memory that was
+ * written after it started: another XCD's L2 would not be kept coherent with
+ * its own, while host memory read after a system-scope acquire is always
+ * current.
+ *
+ * Opens are two-pass (verify first, then decrypt): a rejected record's bytes
+ * are never written back.  Records longer than WORKER_MAX_LEN, or any setup
+ * failure, return NOISE_ERROR_NOT_APPLICABLE and the caller takes the
+ * regular launch path.  NOISE_AEAD_WORKER=0 disables the worker.
+ */
+#include "launch.h"
+#include "chachapoly.hip"
+#define NA_NO_SETUP_KERNELS
+#include "aesgcm.hip"
+#include <cstddef>
+#include <emmintrin.h>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+namespace na {
+
+constexpr uint32_t WORKER_MAX_LEN = 65535 - 16; /* whole records only */
+constexpr uint32_t WORKER_MAX_AD = 256;
+/* data area: ChaCha key (32 B) || AD (padded to 16) || record || tag */
+constexpr uint32_t WORKER_DATA = 32 + WORKER_MAX_AD + 65536 + 64;
+/* AES-GCM contexts the worker keeps in LDS (an echo session uses two) */
+constexpr int WORKER_CTX_SLOTS = 2;
+constexpr uint32_t WORKER_CTX_BYTES = offsetof(AesCtx, tab8); /* rk, H, H^1..H^4 */
+
+/* The request slot (host pinned, fine-grained).  The request header is four
+   16-byte chunks, each starting with the request's sequence number; the host
+   writes each chunk with one 16-byte store after the data area, and the
+   worker takes the header only when all four chunks carry the same new
+   number — one read round trip, no torn header.  The worker's words sit on
+   their own 128-B line. */
+struct alignas(128) WorkerSlot {
+    /* host -> worker */
+    uint32_t c0[4];    /* seq, op | ct << 8, len, ad_len */
+    uint32_t c1[4];    /* seq, nonce lo, nonce hi, cipher */
+    uint32_t c2[4];    /* seq, ctx lo, ctx hi, stop */
+    uint32_t c3[4];    /* seq, ctx generation, 0, 0 */
+    uint8_t pad0[128 - 64];
+    /* worker -> host */
+    uint64_t done;     /* last request completed */
+    uint32_t status;   /* 0 ok, 1 MAC failure */
+    uint32_t exiting;  /* the worker is leaving (or has left) */
+    uint32_t stamps[8]; /* debug: s_memrealtime (10 ns) of the last request's phases */
+    uint8_t pad1[128 - 48];
+};
+static_assert(sizeof(WorkerSlot) == 256, "slot layout");
+
+#define NA_SYS_LOAD(p) __hip_atomic_load((p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+#define NA_SYS_STORE(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM)
+
+/* lanes per ChaChaPoly record: one ChaCha block per lane where it fits
+   (a single step), 4..64 */
+NA_DEV uint32_t worker_lanes(uint32_t len)
+{
+    const uint32_t blocks = (len + 63) / 64 + 1;
+    uint32_t k = 4;
+    while (k < 64 && k < blocks) k <<= 1;
+    return k;
+}
+
+template <int K>
+NA_DEV bool worker_chacha(bool open, const RecView &rv)
+{
+    const int lane = (int)(threadIdx.x & 63);
+    if (lane >= K) return true; /* one record: lanes 0..K-1 of wave 0 */
+    if (!open) {
+        seal_il<K, false>(rv, lane);
+        return true;
+    }
+    return open_il<K, false>(rv, lane); /* verify first, then decrypt */
+}
+
+/* One 16-byte system-coherent load (a single request: the chunk is read
+   whole, never half before and half after the host's 16-byte store). */
+NA_DEV uint4 load_sys16(const uint32_t *p)
+{
+    uint4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                 : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+NA_DEV uint32_t now10ns() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+
+/* 256 threads.  last: the last request already served; idle/lifetime in
+   s_memrealtime ticks (100 MHz). */
+__global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *data, uint32_t last,
+                                                   uint64_t idle, uint64_t lifetime)
+{
+    __shared__ uint32_t te[256], sb[256];
+    __shared__ __attribute__((aligned(16))) uint8_t cbuf[WORKER_CTX_SLOTS][WORKER_CTX_BYTES];
+    __shared__ uint64_t ctag[WORKER_CTX_SLOTS]; /* host address of the cached context */
+    __shared__ uint32_t cgen[WORKER_CTX_SLOTS], cuse[WORKER_CTX_SLOTS];
+    __shared__ uint32_t hdr[16];
+    __shared__ uint32_t verdict, s_cmd; /* s_cmd: 0 wait, 1 serve, 2 leave */
+    __shared__ __attribute__((aligned(16))) uint8_t buf[WORKER_DATA];
+    const uint32_t t = threadIdx.x;
+    aes_table_entry(t, sb[t], te[t]);
+    if (t < WORKER_CTX_SLOTS) {
+        ctag[t] = 0;
+        cgen[t] = 0;
+        cuse[t] = 0;
+    }
+    const uint64_t born = __builtin_amdgcn_s_memrealtime();
+    uint64_t quiet = born;
+    bool leaving = false;
+    uint32_t tick = 0;
+    for (;;) {
+        uint32_t t_seen = 0;
+        if (t < 64) { /* wave 0 polls: lanes 0..3 read one header chunk each */
+            uint4 c = make_uint4(0, 0, 0, 0);
+            if (t < 4) c = load_sys16(slot->c0 + 4 * t);
+            const uint32_t s0 = __shfl((int)c.x, 0, 64), s1 = __shfl((int)c.x, 1, 64);
+            const uint32_t s2 = __shfl((int)c.x, 2, 64), s3 = __shfl((int)c.x, 3, 64);
+            const uint32_t stop = __shfl((int)c.w, 2, 64);
+            const bool fresh = s0 != last && s0 == s1 && s0 == s2 && s0 == s3;
+            if (t < 4) {
+                hdr[4 * t] = c.x; hdr[4 * t + 1] = c.y; hdr[4 * t + 2] = c.z; hdr[4 * t + 3] = c.w;
+            }
+            if (t == 0) {
+                uint32_t cmd = 0;
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                if (fresh) {
+                    cmd = 1;
+                } else if (leaving) {
+                    cmd = 2;
+                } else if (stop || now - quiet > idle || now - born > lifetime) {
+                    /* announce, then poll once more: a request posted before
+                       that poll is served; one posted after it finds
+                       `exiting` set and the host starts a new worker */
+                    NA_SYS_STORE(&slot->exiting, 1u);
+                    leaving = true;
+                } else {
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                s_cmd = cmd;
+                t_seen = (uint32_t)now;
+            }
+        }
+        __syncthreads();
+        const uint32_t cmd = s_cmd;
+        if (cmd == 2) break;
+        if (cmd == 0) {
+            __syncthreads();
+            continue;
+        }
+        /* serve request hdr[0]: the data area was written before the header;
+           the acquire orders the reads below after the header's */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const uint32_t seq = hdr[0], op = hdr[1] & 0xff, ct = (hdr[1] >> 8) & 1;
+        const uint32_t len = hdr[2], ad_len = hdr[3];
+        const uint64_t nonce = (uint64_t)hdr[5] | ((uint64_t)hdr[6] << 32);
+        const uint32_t cipher = hdr[7];
+        const uint64_t ctx_addr = (uint64_t)hdr[9] | ((uint64_t)hdr[10] << 32);
+        const uint32_t gen = hdr[13];
+        const uint32_t ad_pad = (ad_len + 15) & ~15u;
+        const uint32_t bytes = 32 + ad_pad + len + 16;
+        const uint32_t t_fence = now10ns();
+        for (uint32_t o = 16 * t; o < bytes; o += 16 * 256)
+            *(uint4 *)(buf + o) = *(const uint4 *)(data + o);
+        int cs = 0;
+        if (cipher == NOISE_CIPHER_AESGCM) { /* the context: cached, or copied into the LRU slot */
+            cs = ctag[0] == ctx_addr && cgen[0] == gen ? 0 : (ctag[1] == ctx_addr && cgen[1] == gen ? 1 : -1);
+            if (cs < 0) {
+                cs = cuse[0] <= cuse[1] ? 0 : 1;
+                const uint8_t *src = (const uint8_t *)ctx_addr;
+                for (uint32_t o = 16 * t; o < WORKER_CTX_BYTES; o += 16 * 256)
+                    *(uint4 *)(cbuf[cs] + o) = *(const uint4 *)(src + o);
+            }
+        }
+        __syncthreads();
+        if (t == 0 && cipher == NOISE_CIPHER_AESGCM) {
+            ctag[cs] = ctx_addr;
+            cgen[cs] = gen;
+            cuse[cs] = ++tick;
+        }
+        const uint32_t t_in = now10ns();
+        uint8_t *key = buf, *ad = buf + 32, *rec = buf + 32 + ad_pad;
+        bool ok = true;
+        if (cipher == NOISE_CIPHER_CHACHAPOLY) {
+            RecView rv;
+            rv.src = rec;
+            rv.dst = rec;
+            rv.ad = ad;
+            rv.key = key;
+            rv.nonce = nonce;
+            rv.len = len;
+            rv.ad_len = ad_len;
+            if (t < 64) {
+                bool r;
+                switch (worker_lanes(len)) {
+                case 4: r = worker_chacha<4>(op, rv); break;
+                case 8: r = worker_chacha<8>(op, rv); break;
+                case 16: r = worker_chacha<16>(op, rv); break;
+                case 32: r = worker_chacha<32>(op, rv); break;
+                default: r = worker_chacha<64>(op, rv); break;
+                }
+                if (t == 0) verdict = r; /* every lane of the group has the verdict */
+            }
+            __syncthreads();
+            ok = verdict != 0;
+        } else {
+            const AesCtx *c = (const AesCtx *)cbuf[cs]; /* fields before tab8 only */
+            const uint4 *h4 = (const uint4 *)c->tab[GCM_LANES - 1];
+            if (ct) ok = op ? gcm_wide_record<true, true>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h4, &verdict, nullptr)
+                            : gcm_wide_record<false, true>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h4, &verdict, nullptr);
+            else ok = op ? gcm_wide_record<true, false>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h4, &verdict, nullptr)
+                         : gcm_wide_record<false, false>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h4, &verdict, nullptr);
+        }
+        __syncthreads();
+        const uint32_t t_done = now10ns();
+        /* results back: seal CT || tag, open the plaintext (only if verified);
+           every storing wave drains its stores, then one system release and
+           the flag (MI355X_MICROARCH.md, inter-workgroup visibility) */
+        const uint32_t out = op ? (ok ? len : 0u) : len + 16;
+        uint8_t *dout = data + 32 + ad_pad;
+        for (uint32_t o = 16 * t; o < ((out + 15) & ~15u); o += 16 * 256)
+            *(uint4 *)(dout + o) = *(const uint4 *)(rec + o);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t t_out = now10ns();
+            slot->status = ok ? 0u : 1u;
+            slot->stamps[0] = t_seen;
+            slot->stamps[1] = t_fence;
+            slot->stamps[2] = t_in;
+            slot->stamps[3] = t_done;
+            slot->stamps[4] = t_out;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            slot->stamps[5] = now10ns();
+            NA_SYS_STORE(&slot->done, (uint64_t)seq);
+        }
+        last = seq;
+        quiet = __builtin_amdgcn_s_memrealtime();
+        /* scrub this record's bytes (and the key) from LDS before the next one */
+        for (uint32_t o = 16 * t; o < bytes; o += 16 * 256) *(uint4 *)(buf + o) = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+    }
+    /* the cached AES-GCM contexts hold key material too */
+    for (uint32_t o = 16 * t; o < WORKER_CTX_SLOTS * WORKER_CTX_BYTES; o += 16 * 256)
+        *(uint4 *)(&cbuf[0][0] + o) = make_uint4(0, 0, 0, 0);
+}
+
+/* ------------------------------------------------------------- host side */
+
+namespace {
+
+struct Worker {
+    std::mutex mu;
+    int state = 0;             /* 0 unknown, 1 usable, -1 disabled */
+    WorkerSlot *slot = nullptr; /* host view */
+    WorkerSlot *dslot = nullptr; /* device view */
+    uint8_t *data = nullptr, *ddata = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t seq = 0;
+    bool launched = false;
+};
+
+constexpr int kMaxDev = 64;
+Worker g_worker[kMaxDev];
+std::once_flag g_atexit_once;
+
+constexpr uint64_t IDLE_TICKS = 200000;       /* 2 ms at 100 MHz */
+constexpr uint64_t LIFETIME_TICKS = 500000000; /* 5 s */
+
+void worker_stop_all()
+{
+    for (int d = 0; d < kMaxDev; ++d) {
+        Worker &w = g_worker[d];
+        std::lock_guard<std::mutex> lk(w.mu);
+        if (w.state != 1 || !w.launched) continue;
+        __atomic_store_n(&w.slot->c2[3], 1u, __ATOMIC_RELEASE); /* stop */
+        (void)hipStreamSynchronize(w.stream);
+        w.launched = false;
+    }
+}
+
+bool worker_enabled()
+{
+    static const int v = [] {
+        const char *e = getenv("NOISE_AEAD_WORKER");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    return v != 0;
+}
+
+int worker_setup(Worker &w)
+{
+    if (w.state) return w.state;
+    w.state = -1;
+    if (hipHostMalloc((void **)&w.slot, sizeof(WorkerSlot) + WORKER_DATA,
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        return -1;
+    memset(w.slot, 0, sizeof(WorkerSlot) + WORKER_DATA);
+    if (hipHostGetDevicePointer((void **)&w.dslot, w.slot, 0) != hipSuccess) return -1;
+    w.data = (uint8_t *)(w.slot + 1);
+    w.ddata = (uint8_t *)(w.dslot + 1);
+    if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess) return -1;
+    std::call_once(g_atexit_once, [] { atexit(worker_stop_all); });
+    w.state = 1;
+    return 1;
+}
+
+int worker_launch(Worker &w)
+{
+    (void)hipStreamSynchronize(w.stream); /* a previous worker has left */
+    __atomic_store_n(&w.slot->exiting, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&w.slot->c2[3], 0u, __ATOMIC_RELEASE); /* stop */
+    hipLaunchKernelGGL(aead_worker, dim3(1), dim3(256), 0, w.stream, w.dslot, w.ddata,
+                       w.seq, IDLE_TICKS, LIFETIME_TICKS);
+    if (hipGetLastError() != hipSuccess) return NOISE_ERROR_SYSTEM;
+    w.launched = true;
+    return NOISE_ERROR_NONE;
+}
+
+} // namespace
+
+
+extern "C" NA_HIDDEN int na_worker_enabled(void) { return worker_enabled() ? 1 : 0; }
+
+namespace {
+
+bool ct_env()
+{
+    static const bool v = [] {
+        const char *e = getenv("NOISE_AEAD_CT_GHASH");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+} // namespace
+
+/* 16-byte chunk store: one aligned SSE store, which the x86-64 hosts of
+   MI355X (AVX-capable) perform atomically, so the worker never sees half of
+   a chunk; the sequence number in every chunk catches a torn header */
+static inline void store_chunk(uint32_t *dst, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    _mm_store_si128((__m128i *)dst, _mm_set_epi32((int)d, (int)c, (int)b, (int)a));
+}
+
+/* One record through the resident worker: data holds len bytes (+ the tag
+   for open) and receives CT || tag (seal) or, verified, the plaintext.  key:
+   the raw ChaCha key; h_ctx / gen: AES-GCM, the pinned host copy of the
+   state's context and the generation it was written at.  Returns
+   NOISE_ERROR_NONE, _MAC_FAILURE, _SYSTEM, or _NOT_APPLICABLE (take the
+   launch path). */
+extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, const void *h_ctx,
+                                         uint32_t gen, uint64_t nonce, const uint8_t *ad,
+                                         size_t ad_len, uint8_t *data, size_t len, int open)
+{
+    if (cipher_id == NOISE_CIPHER_AESGCM && !h_ctx) return NOISE_ERROR_NOT_APPLICABLE;
+    if (!worker_enabled() || len > WORKER_MAX_LEN || ad_len > WORKER_MAX_AD)
+        return NOISE_ERROR_NOT_APPLICABLE;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return NOISE_ERROR_NOT_APPLICABLE;
+    Worker &w = g_worker[dev];
+    std::lock_guard<std::mutex> lk(w.mu);
+    if (worker_setup(w) != 1) return NOISE_ERROR_NOT_APPLICABLE;
+    void *d_hctx = nullptr;
+    if (h_ctx && hipHostGetDevicePointer(&d_hctx, (void *)h_ctx, 0) != hipSuccess)
+        return NOISE_ERROR_NOT_APPLICABLE;
+    const size_t ad_pad = (ad_len + 15) & ~(size_t)15;
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) memcpy(w.data, key, 32);
+    if (ad_len) memcpy(w.data + 32, ad, ad_len);
+    memcpy(w.data + 32 + ad_pad, data, len + (open ? 16 : 0));
+    WorkerSlot *s = w.slot;
+    if (!w.launched || __atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE)) {
+        const int rc = worker_launch(w);
+        if (rc) return rc;
+    }
+    const uint32_t k = ++w.seq;
+    const uint64_t ctx = (uint64_t)(uintptr_t)d_hctx;
+    __atomic_thread_fence(__ATOMIC_RELEASE); /* the data area before the header */
+    store_chunk(s->c0, k, (open ? 1u : 0u) | (ct_env() ? 1u << 8 : 0u), (uint32_t)len, (uint32_t)ad_len);
+    store_chunk(s->c1, k, (uint32_t)nonce, (uint32_t)(nonce >> 32), (uint32_t)cipher_id);
+    store_chunk(s->c2, k, (uint32_t)ctx, (uint32_t)(ctx >> 32), 0u);
+    store_chunk(s->c3, k, gen, 0u, 0u);
+    uint64_t spins = 0;
+    while (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
+        __builtin_ia32_pause();
+        if ((++spins & 1023) == 0 && __atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE) &&
+            __atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
+            /* the worker left before it took k: start one at k - 1 */
+            if (hipStreamSynchronize(w.stream) != hipSuccess) return NOISE_ERROR_SYSTEM;
+            if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == k) break;
+            w.seq = k - 1;
+            const int rc = worker_launch(w);
+            w.seq = k;
+            if (rc) return rc;
+        }
+        if (spins > (1ull << 32)) return NOISE_ERROR_SYSTEM; /* never in practice */
+    }
+    const int st = s->status ? NOISE_ERROR_MAC_FAILURE : NOISE_ERROR_NONE;
+    uint8_t *res = w.data + 32 + ad_pad;
+    if (!open) memcpy(data, res, len + 16);
+    else if (st == NOISE_ERROR_NONE) memcpy(data, res, len);
+    explicit_bzero(w.data, 32 + ad_pad + len + 16);
+    return st;
+}
+
+/* Test hook: the phase stamps of this device's last worker request, in
+   10-ns ticks relative to the moment the worker saw it: [0] fence done, [1]
+   record and context in LDS, [2] computed, [3] results written, [4] release
+   done; n = 5. */
+extern "C" void noise_aead_debug_worker_stamps(uint32_t *out, int n)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
+    const WorkerSlot *s = g_worker[dev].slot;
+    for (int i = 0; i < n && i < 5; ++i) out[i] = s ? s->stamps[i + 1] - s->stamps[0] : 0;
+}
+
+} // namespace na
