@@ -64,6 +64,11 @@ hipError_t hipMemcpyAsync(void *dst, const void *src, size_t n, hipMemcpyKind ki
     return hipSuccess;
 }
 
+hipError_t hipMemcpy(void *dst, const void *src, size_t n, hipMemcpyKind kind)
+{
+    return hipMemcpyAsync(dst, src, n, kind, NULL);
+}
+
 hipError_t hipMemsetAsync(void *dst, int v, size_t n, hipStream_t s)
 {
     (void)s;
