@@ -159,7 +159,9 @@ int main(int argc, char **argv)
     const bool persist = argc > 3 ? atoi(argv[3]) != 0 : true;
     const double valu = 8192.0; /* SQ_INSTS_VALU per wave-job (profiles/traffic_c2.json) */
     const uint32_t L = 1400, SI = 1408, SO = 1536;
-    for (uint32_t N : {65536u, 524288u}) {
+    const bool big_first = argc > 4 && atoi(argv[4]) != 0; /* clock hysteresis check */
+    const uint32_t order[2] = {big_first ? 524288u : 65536u, big_first ? 65536u : 524288u};
+    for (uint32_t N : order) {
         if (only && N != only) continue;
         uint8_t *pa, *ca, *cb, *back, *key, *st;
         uint64_t *nb;
