@@ -393,6 +393,9 @@ def parse_args():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--lanes", type=int, default=0, help="lanes per record (0 = library default)")
     ap.add_argument("--sets", type=int, default=4, help="rotating batch sets (> MALL)")
+    ap.add_argument("--settle-ms", type=float, default=500.0,
+                    help="untimed back-to-back steps before the warmup, in ms of wall clock "
+                         "(the sustained-load clock, see settle()); 0 = off")
     ap.add_argument("--align", type=int, default=SLOT_ALIGN, choices=(16, 64, 128, 256),
                     help="record slot alignment of the device batch (strides roundup(len, align), "
                          "roundup(len + 16, align))")
@@ -513,6 +516,8 @@ def main():
                    "payload_bytes_per_step": int(payload_step), "parallelism": f"records x{world}",
                    "streams": len(wl.streams), "mode": args.mode, "events": args.events,
                    "open_reads_set_sealed_steps_before": wl.lag,
+                   "settle": {"ms": args.settle_ms, "steps": wl.settle_steps,
+                              "s": round(wl.settle_s, 3)},
                    "open_order": ("verify-first (NOISE_AEAD_FLAG_VERIFY_FIRST: authenticate, then "
                                   "decrypt verified records)" if args.verify_first else
                                   "one pass (decrypt while authenticating; a rejected record's "
@@ -545,6 +550,35 @@ def main():
         except Exception as e:  # reported, never fatal to the GPU number
             result["cpu_baseline"] = {"error": str(e)}
     finish(args, result, rank, world, dist)
+
+
+def settle(torch, dev, stream, ms, step):
+    """Run the workload's own step back to back for `ms` of wall clock before
+    the warmup steps, keeping 8-32 steps queued (no idle GPU between chunks),
+    so the timed steps see the clock the chip holds under sustained load.
+    Under a VALU-dense load MI355X first boosts, drops to ~1.9 GHz after
+    ~5 ms, then climbs back to ~2.4 GHz over ~0.1-0.3 s (C2-shaped duplex
+    launch, tools/microbench/timeline3: 2.03 GHz after 10 launches, 1.90 after
+    40, 2.33 after 200, 2.44 after 2000; profiles/r03/clock_vs_warmup.log).
+    Returns (steps run, seconds)."""
+    if ms <= 0:
+        return 0, 0.0
+    t0 = time.perf_counter()
+    t_end = t0 + ms * 1e-3
+    n, chunk, prev = 0, 16, None
+    while True:
+        for _ in range(chunk):
+            step(n)
+            n += 1
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        if prev is not None:
+            prev.synchronize()  # the chunk before this one is done: 1-2 chunks stay queued
+        prev = ev
+        if time.perf_counter() >= t_end:
+            break
+    torch.cuda.synchronize(dev)
+    return n, time.perf_counter() - t0
 
 
 class UniformWork:
@@ -634,20 +668,26 @@ class UniformWork:
                            **self._common())
         return A.dev_duplex(self.cipher, sj, oj, self.sp)
 
+    def untimed_step(self, w):
+        """Step w outside the timed region (settle, warmup): the same launches."""
+        b, bo = w % self.args.sets, (w - self.lag) % self.args.sets
+        if self.duplex:
+            assert self.step_duplex(b, bo) == 0
+        else:
+            assert self.seal(b) == 0
+            assert self.open_(bo) == 0
+
     def timed(self, steps, warmup, dist):
-        """Warm up, then time exactly `steps` steps between barrier +
+        """Settle (see settle()), warm up, then time exactly `steps` steps between barrier +
         synchronize on both sides; returns this rank's seconds.  Also sets
         launch_ms (HIP events on the launch stream)."""
         torch, dev, sets = self.torch, self.dev, self.args.sets
         for b in range(sets):
             assert self.seal(b) == 0
+        self.settle_steps, self.settle_s = settle(torch, dev, self.stream, self.args.settle_ms,
+                                                  self.untimed_step)
         for w in range(warmup):
-            b, bo = w % sets, (w - self.lag) % sets
-            if self.duplex:
-                assert self.step_duplex(b, bo) == 0
-            else:
-                assert self.seal(b) == 0
-                assert self.open_(bo) == 0
+            self.untimed_step(w)
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()
@@ -933,7 +973,11 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
             join[open_].record(side)
             main_s.wait_event(join[open_])
 
+    settled = [0, 0.0]
+
     def timed(d):
+        settled[:] = settle(torch, dev, torch.cuda.current_stream(dev), args.settle_ms,
+                            lambda n: step())
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize(dev)
@@ -1011,7 +1055,8 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
         "config": {"workload": cfg["workload"], "config": "c5", "records_per_gpu": R,
                    "states_per_gpu": S, "payload_bytes_per_step": int(2 * payload * world),
                    "streams": 2 if side is not None else 1,
-                   "parallelism": f"states x{world}"},
+                   "parallelism": f"states x{world}",
+                   "settle": {"ms": args.settle_ms, "steps": settled[0], "s": round(settled[1], 3)}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": pmc.get("hbm_bytes_per_launch"),

@@ -385,6 +385,9 @@ void noise_aead_debug_batch_stats(uint64_t *rounds, uint64_t *dispatched);
  *   resident single-record worker's last request on the current device:
  *   fence, inputs in LDS, computed, results written, released (n <= 5). */
 void noise_aead_debug_worker_stamps(uint32_t *out, int n);
+/* noise_aead_debug_worker_clock_mhz: the shader clock of that request's
+ *   compute phase (s_memtime cycles / s_memrealtime time), 0 if none. */
+double noise_aead_debug_worker_clock_mhz(void);
 void *noise_aead_debug_last_freed_ctx(size_t *bytes);
 
 /* Default lanes per record the library picks for a batch of n records. */

@@ -308,6 +308,68 @@ NA_DEV void poly_close(Fe acc, int k, const Mul &mr, const Mul &mfinal, uint64_t
     fe_finish(acc, s, tag);
 }
 
+/* Wide groups (K >= 16) whose record fits one step (each lane holds at most
+   one unit, the single-record and small-batch case): no r^(4K-3) jump and
+   no per-lane power of r.  Lane k < K-1 holds a full unit at position
+   p = K-2-k from the right (h_p: Horner over its blocks, the AD first on the
+   unit-0 lane), lane K-1 the last unit and the length block.  With R = r^4,
+     S = sum_p h_p R^p   (a right-aligned tree over the lanes: level L adds
+                          lane k-L's value times R^L into lane k),
+     poly = S r^(q+2) + h_last r,
+   q+2 = the blocks after lane K-2's last block plus the final r.  log2(K)
+   multiplies deep instead of ~2 log2(4K) squarings and multiplies per lane
+   (fe_pow), for the latency of one record on one wave.  Every lane of the
+   group gets the tag. */
+template <int K>
+NA_DEV void poly_tree_close(Fe acc, int k, const Fe &r, const Mul &mr, uint32_t J, uint32_t q,
+                            uint64_t ad_len, uint64_t len, const uint32_t s[4], uint32_t tag[4])
+{
+    const int lane = (int)(threadIdx.x & 63), gbase = lane & ~(K - 1);
+    if (k == K - 1) {
+        acc = fe_mul(acc, mr);
+        fe_add_block(acc, (uint32_t)ad_len, (uint32_t)(ad_len >> 32), (uint32_t)len,
+                     (uint32_t)(len >> 32));
+    }
+    const Fe r2 = fe_mul(r, mr);
+    const Mul m2 = mk_mul(r2);
+    const Fe r4 = fe_mul(r2, m2);
+    const Mul m4 = mk_mul(r4);
+    Fe v = (k == K - 1) ? fe_zero() : acc;
+    const int p = K - 2 - k;
+    const uint32_t full = J ? J - 1 : 0; /* lanes holding a full unit */
+    Mul mR = m4;
+#pragma unroll
+    for (int L = 1; L < K - 1; L <<= 1) {
+        if (!__any((uint32_t)L < full)) break; /* no group has a level this wide */
+        Fe w;
+        const int src = lane - L;
+        w.l0 = (uint32_t)__shfl((int)v.l0, src, 64);
+        w.l1 = (uint32_t)__shfl((int)v.l1, src, 64);
+        w.l2 = (uint32_t)__shfl((int)v.l2, src, 64);
+        w.l3 = (uint32_t)__shfl((int)v.l3, src, 64);
+        w.l4 = (uint32_t)__shfl((int)v.l4, src, 64);
+        const Fe t = fe_mul(w, mR);
+        if (p >= 0 && (p & (2 * L - 1)) == 0 && k - L >= 0) v = fe_carry(fe_add(v, t));
+        if (2 * L < K - 1) mR = mk_mul(fe_mul(mul_fe(mR), mR)); /* R^(2L) */
+    }
+    /* lane K-1: S from lane K-2, then S r^(q+2) + h_last r */
+    Fe S;
+    const int from = gbase + K - 2;
+    S.l0 = (uint32_t)__shfl((int)v.l0, from, 64);
+    S.l1 = (uint32_t)__shfl((int)v.l1, from, 64);
+    S.l2 = (uint32_t)__shfl((int)v.l2, from, 64);
+    S.l3 = (uint32_t)__shfl((int)v.l3, from, 64);
+    S.l4 = (uint32_t)__shfl((int)v.l4, from, 64);
+    /* r^(q+2), q = 1..4: r^3, r^4, r^5, r^6 (any value when there is no full unit) */
+    const Fe rq = (q <= 2) ? ((q == 2) ? r4 : fe_mul(r2, mr)) : fe_mul(r4, (q == 3) ? mr : m2);
+    Fe T = fe_add(fe_mul(acc, mr), fe_mul(S, mk_mul(rq)));
+    uint32_t t4[4];
+    fe_finish(T, s, t4);
+    const int last = gbase + K - 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tag[i] = (uint32_t)__shfl((int)t4[i], last, 64);
+}
+
 /* The key stream of lane slot v of a staged step.  Slots before block 0
    (v < 0: the end alignment's padding, 1 of 24 at 1400 B, 3 of 20 at 1024 B)
    carry no block, and their lanes run the step switched off instead of
@@ -340,6 +402,7 @@ NA_DEV void seal_il(const RecView &rv, int k)
     const uint32_t len = rv.len;
     const GroupCtx<K> g = group_ctx<K>(len);
     const int gbase = (int)(threadIdx.x & 63) & ~(K - 1);
+    const bool tree = K >= 16 && g.steps == 1; /* poly_tree_close */
 
     Fe acc = fe_zero(), r;
     Mul mr, mjump, mfinal;
@@ -361,7 +424,7 @@ NA_DEV void seal_il(const RecView &rv, int k)
         if (m == 0) {
             poly_key_bcast(x, gbase + (int)g.o, r, s);
             mr = mk_mul(r);
-            poly_powers<K>(r, k, g.q, mjump, mfinal);
+            if (!tree) poly_powers<K>(r, k, g.q, mjump, mfinal);
             /* unit 0 (block 1) sits in lane (o+1) % K; with no units, lane K-1 */
             const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
             if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
@@ -387,7 +450,8 @@ NA_DEV void seal_il(const RecView &rv, int k)
         poly_unit(acc, seen ? mjump : mr, mr, w, (nb + 15) / 16);
     }
     uint32_t tag[4];
-    poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
+    if (tree) poly_tree_close<K>(acc, k, r, mr, g.J, g.q, rv.ad_len, len, s, tag);
+    else poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
     if (k == K - 1) tail_out<FAST, true>(rv.dst, g.J, len, w, tag);
 }
 
@@ -409,6 +473,7 @@ NA_DEV bool open_il_1p(const RecView &rv, int k)
     const uint32_t len = rv.len;
     const GroupCtx<K> g = group_ctx<K>(len);
     const int gbase = (int)(threadIdx.x & 63) & ~(K - 1);
+    const bool tree = K >= 16 && g.steps == 1; /* poly_tree_close */
     const uint32_t tail = g.J ? len - 64 * (g.J - 1) : 0; /* bytes of unit J-1 */
 
     Fe acc = fe_zero(), r;
@@ -431,7 +496,7 @@ NA_DEV bool open_il_1p(const RecView &rv, int k)
         if (m == 0) {
             poly_key_bcast(x, gbase + (int)g.o, r, s);
             mr = mk_mul(r);
-            poly_powers<K>(r, k, g.q, mjump, mfinal);
+            if (!tree) poly_powers<K>(r, k, g.q, mjump, mfinal);
             const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
             if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
         }
@@ -457,7 +522,8 @@ NA_DEV bool open_il_1p(const RecView &rv, int k)
         tail_out<true, false>(rv.dst, g.J, len, w, nullptr);
     }
     uint32_t tag[4], got[4];
-    poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
+    if (tree) poly_tree_close<K>(acc, k, r, mr, g.J, g.q, rv.ad_len, len, s, tag);
+    else poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
     tag_in<true>(rv.src, len, got); /* the tag bytes are never written */
     const bool ok = tag_equal(tag, got);
     if (ok || rv.dst != rv.src) return ok;
@@ -507,6 +573,7 @@ NA_DEV bool open_il(const RecView &rv, int k, AuthRing ring = AuthRing{})
     const uint32_t len = rv.len;
     const GroupCtx<K> g = group_ctx<K>(len);
     const int gbase = (int)(threadIdx.x & 63) & ~(K - 1);
+    const bool tree = K >= 16 && g.steps == 1; /* poly_tree_close */
 
     /* step-0 key stream: block 0 on lane o, data on the others (kept) */
     const int v0 = k - (int)g.o;
@@ -517,7 +584,7 @@ NA_DEV bool open_il(const RecView &rv, int k, AuthRing ring = AuthRing{})
     poly_key_bcast(x0, gbase + (int)g.o, r, s);
     const Mul mr = mk_mul(r);
     Mul mjump, mfinal;
-    poly_powers<K>(r, k, g.q, mjump, mfinal);
+    if (!tree) poly_powers<K>(r, k, g.q, mjump, mfinal);
     Fe acc = fe_zero();
     const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
     if (k == k0 && rv.ad_len) poly_ad(acc, mr, rv.ad, rv.ad_len);
@@ -594,7 +661,8 @@ NA_DEV bool open_il(const RecView &rv, int k, AuthRing ring = AuthRing{})
     }
     }
     uint32_t tag[4], got[4];
-    poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
+    if (tree) poly_tree_close<K>(acc, k, r, mr, g.J, g.q, rv.ad_len, len, s, tag);
+    else poly_close<K>(acc, k, mr, mfinal, rv.ad_len, len, s, tag);
     tag_in<FAST>(rv.src, len, got);
     if (!tag_equal(tag, got)) return false; /* identical verdict on the group */
 

@@ -212,6 +212,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
             cuse[cs] = ++tick;
         }
         const uint32_t t_in = now10ns();
+        const uint64_t c_in = __builtin_amdgcn_s_memtime();
         uint8_t *key = buf, *ad = buf + 32, *rec = buf + 32 + ad_pad;
         bool ok = true;
         if (cipher == NOISE_CIPHER_CHACHAPOLY) {
@@ -246,6 +247,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
         }
         __syncthreads();
         const uint32_t t_done = now10ns();
+        const uint32_t c_run = (uint32_t)(__builtin_amdgcn_s_memtime() - c_in); /* shader cycles */
         /* results back: seal CT || tag, open the plaintext (only if verified);
            every storing wave drains its stores, then one system release and
            the flag (MI355X_MICROARCH.md, inter-workgroup visibility) */
@@ -263,6 +265,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
             slot->stamps[2] = t_in;
             slot->stamps[3] = t_done;
             slot->stamps[4] = t_out;
+            slot->stamps[6] = c_run;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             slot->stamps[5] = now10ns();
@@ -447,6 +450,17 @@ extern "C" void noise_aead_debug_worker_stamps(uint32_t *out, int n)
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
     const WorkerSlot *s = g_worker[dev].slot;
     for (int i = 0; i < n && i < 5; ++i) out[i] = s ? s->stamps[i + 1] - s->stamps[0] : 0;
+}
+
+/* Test hook: the shader clock (MHz) of the last worker request's compute
+   phase (s_memtime cycles over s_memrealtime time). */
+extern "C" double noise_aead_debug_worker_clock_mhz(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0.0;
+    const WorkerSlot *s = g_worker[dev].slot;
+    if (!s || s->stamps[3] == s->stamps[2]) return 0.0;
+    return (double)s->stamps[6] / ((double)(s->stamps[3] - s->stamps[2]) * 0.01);
 }
 
 } // namespace na

@@ -42,6 +42,7 @@ int main(int argc, char **argv)
     for (size_t i = 0; i < len; ++i) ref[i] = (uint8_t)(i * 13);
     double *te = malloc(iters * sizeof(double)), *td = malloc(iters * sizeof(double));
     double ph[5] = {0, 0, 0, 0, 0}; /* resident-worker phase stamps (us), decrypt calls */
+    double mhz = 0;                 /* the worker's shader clock while computing */
     int ok = 1;
     for (int it = -50; it < iters; ++it) { /* 50 untimed warm-up messages */
         NoiseBuffer b;
@@ -59,6 +60,7 @@ int main(int argc, char **argv)
             uint32_t st[5];
             noise_aead_debug_worker_stamps(st, 5);
             for (int i = 0; i < 5; ++i) ph[i] += st[i] * 0.01 / iters;
+            mhz += noise_aead_debug_worker_clock_mhz() / iters;
         }
     }
     qsort(te, iters, sizeof(double), cmp_d);
@@ -67,9 +69,9 @@ int main(int argc, char **argv)
            "\"encrypt_us_p50\": %.2f, \"encrypt_us_p99\": %.2f, "
            "\"decrypt_us_p50\": %.2f, \"decrypt_us_p99\": %.2f, "
            "\"worker_phase_us\": {\"fence\": %.2f, \"inputs\": %.2f, \"computed\": %.2f, "
-           "\"written\": %.2f, \"released\": %.2f}, \"ok\": %s}\n",
+           "\"written\": %.2f, \"released\": %.2f}, \"worker_clock_mhz\": %.0f, \"ok\": %s}\n",
            name, len, iters, te[iters / 2], te[iters * 99 / 100], td[iters / 2],
-           td[iters * 99 / 100], ph[0], ph[1], ph[2], ph[3], ph[4], ok ? "true" : "false");
+           td[iters * 99 / 100], ph[0], ph[1], ph[2], ph[3], ph[4], mhz, ok ? "true" : "false");
     noise_cipherstate_free(tx);
     noise_cipherstate_free(rx);
     return ok ? 0 : 1;
