@@ -1,0 +1,14 @@
+# The worker's latency-first ChaChaPoly path: its tests, the drop-in suites
+# (the reference's own single calls), then latency.
+set -eu
+R=$GRAFT_REPO_ROOT; cd $R
+O=$R/gpurun_out/r03_worker2; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_worker.py tests/test_dropin.py tests/test_echo_dropin.py tests/test_gpu_hardening.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+: > $O/latency.jsonl
+for c in chachapoly aesgcm; do
+  for n in 64 1024 1400 4096 16384; do
+    timeout -k 10 60 ./tools/latency $c $n 2000 >> $O/latency.jsonl
+  done
+done
+cat $O/latency.jsonl
