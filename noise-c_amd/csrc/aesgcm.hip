@@ -703,18 +703,17 @@ NA_DEV void gcm_ctr_lane(const uint8_t *TE, const uint32_t *rk, uint32_t tpl, co
     }
 }
 
-/* One 1024-thread workgroup of a uniform staged job: records
-   [blk * 256, blk * 256 + 256). */
+/* This thread's record of block blk (records [blk * 256, blk * 256 + 256))
+   of a uniform staged job, with the T-tables at TE and the state's
+   multiply-by-H^4 table and round keys (h4_lds, rk) in LDS. */
 template <bool OPEN, bool CT>
-NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
+NA_DEV void gcm_staged_rec(const UniformArgs &a, const uint8_t *TE, const uint4 *h4_lds,
+                           const uint32_t *rk, uint32_t blk)
 {
     constexpr int K = GCM_LANES;
-    const uint8_t *TE = (const uint8_t *)&L.te[0][0][0];
     const uint32_t rec0 = blk * (uint32_t)GCM_WG_RECS;
     const uint32_t st = rec0 / a.rps; /* one state per workgroup (host-checked) */
     const AesCtx *ctx = (const AesCtx *)a.keys + st;
-    gcm_lds_fill(L, ctx);
-
     const uint32_t rec = rec0 + threadIdx.x / K;
     if (rec >= a.n_records) return;
     const uint32_t lane = threadIdx.x & 63;
@@ -738,10 +737,10 @@ NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
         for (int w = 0; w < 4; ++w) h4n[w] = ctx->hn[K - 1][w];
     }
     uint32_t acc[4] = {0, 0, 0, 0};
-    const AesPre pre = aes_pre_lds(TE, L.rk, tpl, n_hi, n_lo);
+    const AesPre pre = aes_pre_lds(TE, rk, tpl, n_hi, n_lo);
 #pragma unroll 1
     for (uint32_t i = c0; i < n; i += K) {
-        if (i != c0) gh_step<CT>(acc, L.h4, h4n);
+        if (i != c0) gh_step<CT>(acc, h4_lds, h4n);
         uint32_t x[4];
         if (i >= A && i < A + M) {
             const uint32_t d = i - A;
@@ -754,7 +753,7 @@ NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
                authenticate here and decrypt after the verdict. */
             if (!OPEN || !a.vf) {
                 uint32_t ks[4], y[4];
-                aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
+                aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
 #pragma unroll
                 for (int w = 0; w < 4; ++w) y[w] = x[w] ^ ks[w];
                 if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(y[0], y[1], y[2], y[3]);
@@ -785,7 +784,7 @@ NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
         for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
     if constexpr (CT) gh_to_nat(acc);
     uint32_t ej[4];
-    aes_ctr_pre(TE, L.rk, tpl, pre, 1u, ej);
+    aes_ctr_pre(TE, rk, tpl, pre, 1u, ej);
     const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
     if (!OPEN) {
         if (l == K - 1) {
@@ -802,7 +801,7 @@ NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
     const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) | (tag[3] ^ got[3])) == 0;
     if (l == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;
     if (a.vf) { /* verified: decrypt now; rejected: nothing was written */
-        if (ok) gcm_ctr_lane(TE, L.rk, tpl, pre, src, dst, len, (c0 + K - (A % K)) % K, M, K);
+        if (ok) gcm_ctr_lane(TE, rk, tpl, pre, src, dst, len, (c0 + K - (A % K)) % K, M, K);
         return;
     }
     if (ok) return;
@@ -818,13 +817,22 @@ NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
     for (uint32_t d = (c0 + K - (A % K)) % K; d < M; d += K) {
         const uint4 v = *(const uint4 *)(dst + 16 * d);
         uint32_t x[4] = {v.x, v.y, v.z, v.w}, ks[4];
-        aes_ctr_pre(TE, L.rk, tpl, pre, 2 + d, ks);
+        aes_ctr_pre(TE, rk, tpl, pre, 2 + d, ks);
 #pragma unroll
         for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
         const uint32_t nb = min(len - 16 * d, 16u);
         if (nb == 16) *(uint4 *)(dst + 16 * d) = make_uint4(x[0], x[1], x[2], x[3]);
         else store16(dst + 16 * d, nb, x);
     }
+}
+
+/* One 1024-thread workgroup of a uniform staged job. */
+template <bool OPEN, bool CT>
+NA_DEV void gcm_staged_wg(const UniformArgs &a, GcmLds &L, uint32_t blk)
+{
+    const uint32_t st = blk * (uint32_t)GCM_WG_RECS / a.rps;
+    gcm_lds_fill(L, (const AesCtx *)a.keys + st);
+    gcm_staged_rec<OPEN, CT>(a, (const uint8_t *)&L.te[0][0][0], L.h4, L.rk, blk);
 }
 
 template <bool OPEN, bool CT>
@@ -856,6 +864,46 @@ __global__ __launch_bounds__(GCM_WG) void gcm_duplex_staged(UniformArgs s, Unifo
     }
     if (open) gcm_staged_wg<true, CT>(o, L, b);
     else gcm_staged_wg<false, CT>(s, L, b);
+}
+
+/* Fused duplex: workgroup b seals block b of job s, then opens block b of
+   job o, on ONE fill of the LDS T-tables (a second slot holds the open
+   job's state: H^4 table and round keys).  Each wave goes on to its open
+   record as soon as its seal record is done, so a CU's SIMDs stay busy
+   through the first half's uneven finish and the workgroup drains once, not
+   twice.  Results are those of the separate kernels (same per-record code). */
+struct GcmLds2 {
+    uint32_t te[2][256][64];
+    uint4 h4[2][GHASH_TAB_ENTRIES];
+    uint32_t rk[2][60];
+};
+
+NA_DEV void gcm_key_fill(uint4 *h4, uint32_t *rk, const AesCtx *ctx)
+{
+    const uint4 *src = (const uint4 *)ctx->tab[GCM_LANES - 1];
+    for (int i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += GCM_WG) h4[i] = src[i];
+    if (threadIdx.x < 60) rk[threadIdx.x] = ctx->rk[threadIdx.x];
+}
+
+template <bool CT>
+__global__ __launch_bounds__(GCM_WG) void gcm_duplex_fused(UniformArgs s, UniformArgs o,
+                                                            uint32_t s_blocks, uint32_t o_blocks)
+{
+    __shared__ GcmLds2 L;
+    const uint32_t b = blockIdx.x;
+    const int t = threadIdx.x;
+    for (int q = t; q < 2 * 256 * 16; q += GCM_WG) {
+        const int reg = q >> 12, row = (q >> 4) & 255, quad = q & 15;
+        const int tab = 2 * reg + (quad >> 3);
+        const uint32_t v = rotr(g_te0[row], 8 * tab);
+        ((uint4 *)&L.te[reg][row][0])[quad] = make_uint4(v, v, v, v);
+    }
+    if (b < s_blocks) gcm_key_fill(L.h4[0], L.rk[0], (const AesCtx *)s.keys + b * (uint32_t)GCM_WG_RECS / s.rps);
+    if (b < o_blocks) gcm_key_fill(L.h4[1], L.rk[1], (const AesCtx *)o.keys + b * (uint32_t)GCM_WG_RECS / o.rps);
+    __syncthreads();
+    const uint8_t *TE = (const uint8_t *)&L.te[0][0][0];
+    if (b < s_blocks) gcm_staged_rec<false, CT>(s, TE, L.h4[0], L.rk[0], b);
+    if (b < o_blocks) gcm_staged_rec<true, CT>(o, TE, L.h4[1], L.rk[1], b);
 }
 
 /* ------------------------------ staged ragged (any mix of states / lengths)

@@ -122,10 +122,25 @@ int aes_uniform(const UniformArgs &a, bool open, bool ct, bool staged, hipStream
     return hip_rc(hipGetLastError());
 }
 
+/* NOISE_AEAD_GCM_DUPLEX=fused | staged selects the duplex kernel (A/B runs) */
+static bool gcm_duplex_fused_on()
+{
+    static const bool v = [] {
+        const char *e = getenv("NOISE_AEAD_GCM_DUPLEX");
+        return e && !strcmp(e, "fused");
+    }();
+    return v;
+}
+
 int aes_duplex(const UniformArgs &a, const UniformArgs &b, bool ct, hipStream_t s)
 {
     const uint32_t sb = (a.n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
     const uint32_t ob = (b.n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
+    if (gcm_duplex_fused_on()) {
+        hipLaunchKernelGGL(ct ? gcm_duplex_fused<true> : gcm_duplex_fused<false>,
+                           dim3(sb > ob ? sb : ob), dim3(GCM_WG), 0, s, a, b, sb, ob);
+        return hip_rc(hipGetLastError());
+    }
     hipLaunchKernelGGL(ct ? gcm_duplex_staged<true> : gcm_duplex_staged<false>, dim3(sb + ob),
                        dim3(GCM_WG), 0, s, a, b, sb, ob);
     return hip_rc(hipGetLastError());

@@ -107,6 +107,175 @@ NA_DEV bool worker_chacha(bool open, const RecView &rv)
     return open_il<K, false>(rv, lane); /* verify first, then decrypt */
 }
 
+/* ---------------------------------------------- latency-first ChaChaPoly
+ *
+ * One record on the whole workgroup, built for the depth of its dependency
+ * chains rather than its instruction count (a lone wave issues about one
+ * instruction per 4.7 cycles, so depth and count both cost time):
+ *  - ChaCha20 four lanes per block (quad q = block q, lane c = column c:
+ *    words c, 4+c, 8+c, 12+c), the diagonal rounds by quad DPP rotations of
+ *    rows b, c, d: ~330 instructions per lane instead of ~1000;
+ *  - Poly1305 one 16-byte block per lane (AD blocks, CT blocks, the length
+ *    block: n of them), right-justified in N = 2^ceil(log2 n) lanes, and the
+ *    polynomial sum_i b_i r^(n-i) as a left-aligned tree: level L sets
+ *    v_j = v_j r^L + v_{j+L} for j = 0 mod 2L (in-wave shuffles below 64,
+ *    LDS for 64 and 128), then * r: log2(n) multiplies deep;
+ *  - open verifies first and writes plaintext only on a match.
+ * Records of up to WFAST_BLOCKS - 1 units with n <= 256 take it
+ * (worker_fast_fits); the result equals seal_il / open_il's bit for bit (the
+ * same Poly1305 value: sum_i b_i r^(n-i+1) mod 2^130-5 + s). */
+constexpr uint32_t WFAST_BLOCKS = 64; /* ChaCha blocks: 4 lanes each on 256 threads */
+
+NA_DEV bool worker_fast_fits(uint32_t len, uint32_t ad_len)
+{
+    const uint32_t blocks = (len + 63) / 64 + 1;
+    const uint32_t n = (ad_len + 15) / 16 + (len + 15) / 16 + 1;
+    return blocks <= WFAST_BLOCKS && n <= 256;
+}
+
+template <int CTRL>
+NA_DEV uint32_t quad_perm(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false); }
+
+/* quad_perm controls: lane i of a quad reads lane perm[i] */
+constexpr int QP_NEXT1 = 0x39; /* [1,2,3,0] */
+constexpr int QP_NEXT2 = 0x4e; /* [2,3,0,1] */
+constexpr int QP_NEXT3 = 0x93; /* [3,0,1,2] */
+
+/* ChaCha20 block `ctr` on the four lanes of a quad; lane c returns words
+   c, 4+c, 8+c, 12+c of the key stream (chacha.c:74-133 layout). */
+NA_DEV void chacha_quad(const uint32_t key[8], uint32_t ctr, uint32_t n_lo, uint32_t n_hi, int c,
+                        uint32_t &oa, uint32_t &ob, uint32_t &oc, uint32_t &od)
+{
+    const uint32_t a0 = c == 0 ? 0x61707865u : c == 1 ? 0x3320646eu : c == 2 ? 0x79622d32u : 0x6b206574u;
+    const uint32_t b0 = c == 0 ? key[0] : c == 1 ? key[1] : c == 2 ? key[2] : key[3];
+    const uint32_t c0 = c == 0 ? key[4] : c == 1 ? key[5] : c == 2 ? key[6] : key[7];
+    const uint32_t d0 = c == 0 ? ctr : c == 1 ? 0u : c == 2 ? n_lo : n_hi;
+    uint32_t a = a0, b = b0, cc = c0, d = d0;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        NA_QR(a, b, cc, d);                                   /* columns */
+        b = quad_perm<QP_NEXT1>(b); cc = quad_perm<QP_NEXT2>(cc); d = quad_perm<QP_NEXT3>(d);
+        NA_QR(a, b, cc, d);                                   /* diagonals */
+        b = quad_perm<QP_NEXT3>(b); cc = quad_perm<QP_NEXT2>(cc); d = quad_perm<QP_NEXT1>(d);
+    }
+    oa = a + a0; ob = b + b0; oc = cc + c0; od = d + d0;
+}
+
+/* 16 bytes at p (16-B aligned LDS), bytes from `n` on cleared */
+NA_DEV void lds_block(const uint8_t *p, uint32_t n, uint32_t w[4])
+{
+    const uint4 v = *(const uint4 *)p;
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int rem = (int)n - 4 * i;
+        w[i] &= rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
+    }
+}
+
+struct FastLds {
+    uint32_t rs[8];          /* r, s (key stream words 0..7 of block 0) */
+    uint32_t v[4][5];        /* the tree's cross-wave partners (levels 64, 128) */
+    uint32_t verdict;
+};
+
+/* rec: len bytes (+ the tag for open) in LDS, 16-B aligned; ad: ad_len bytes
+   (16-B aligned, padded).  256 threads, every one calls this. */
+template <bool OPEN>
+NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len, uint32_t len,
+                               const uint8_t *key8, uint64_t nonce, FastLds &F)
+{
+    const int t = (int)threadIdx.x, lane = t & 63, c = t & 3;
+    const uint32_t q = (uint32_t)t >> 2; /* ChaCha block */
+    uint32_t key[8];
+    load_key(key8, key);
+    const uint32_t n_lo = (uint32_t)nonce, n_hi = (uint32_t)(nonce >> 32);
+    const uint32_t J = (len + 63) / 64; /* data blocks 1..J */
+    uint32_t ks[4] = {0, 0, 0, 0};
+    if (q <= J) chacha_quad(key, q, n_lo, n_hi, c, ks[0], ks[1], ks[2], ks[3]);
+    if (q == 0) { F.rs[c] = ks[0]; F.rs[4 + c] = ks[1]; }
+    /* data words 64(q-1) + 4c + 16i, i = 0..3: key stream word 4i + c */
+    uint32_t pt[4] = {0, 0, 0, 0};
+    if (q >= 1 && q <= J) {
+        uint32_t *w = (uint32_t *)(rec + 64 * (q - 1) + 4 * c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            pt[i] = w[4 * i] ^ ks[i];
+            if (!OPEN) w[4 * i] = pt[i]; /* CT; bytes past len are overwritten by the tag */
+        }
+    }
+    __syncthreads();
+    /* Poly1305 block of this lane, right-justified in N lanes */
+    const uint32_t a = (ad_len + 15) / 16, m = (len + 15) / 16, n = a + m + 1;
+    const uint32_t N = n <= 1 ? 1u : 1u << (32 - __builtin_clz(n - 1));
+    const int i = t - (int)(N - n);
+    Fe v = fe_zero();
+    if (i >= 0 && (uint32_t)i < n) {
+        uint32_t b[4];
+        if ((uint32_t)i < a) {
+            lds_block(ad + 16 * i, ad_len - 16 * i, b);
+        } else if ((uint32_t)i < a + m) {
+            const uint32_t j = (uint32_t)i - a;
+            lds_block(rec + 16 * j, len - 16 * j, b);
+        } else {
+            b[0] = ad_len; b[1] = 0; b[2] = len; b[3] = 0;
+        }
+        fe_add_block(v, b[0], b[1], b[2], b[3]);
+    }
+    const Fe r = fe_clamp_r(F.rs[0], F.rs[1], F.rs[2], F.rs[3]);
+    Mul mP = mk_mul(r); /* r^L */
+#pragma unroll 1 /* barriers inside: hipcc does not unroll it */
+    for (uint32_t L = 1; L < 256; L <<= 1) {
+        if (L >= N) break; /* uniform */
+        const bool recv = (t & (2 * L - 1)) == 0;
+        Fe w;
+        if (L < 64) {
+            w.l0 = (uint32_t)__shfl((int)v.l0, lane + (int)L, 64);
+            w.l1 = (uint32_t)__shfl((int)v.l1, lane + (int)L, 64);
+            w.l2 = (uint32_t)__shfl((int)v.l2, lane + (int)L, 64);
+            w.l3 = (uint32_t)__shfl((int)v.l3, lane + (int)L, 64);
+            w.l4 = (uint32_t)__shfl((int)v.l4, lane + (int)L, 64);
+        } else {
+            /* partner t + L sits in another wave: through LDS */
+            if (lane == 0 && (t & (int)(2 * L - 1)) == (int)L) {
+                const int slot = t >> 6;
+                F.v[slot][0] = v.l0; F.v[slot][1] = v.l1; F.v[slot][2] = v.l2;
+                F.v[slot][3] = v.l3; F.v[slot][4] = v.l4;
+            }
+            __syncthreads();
+            const int slot = min((t + (int)L) >> 6, 3); /* receivers: 1, 2 or 3 */
+            w = Fe{F.v[slot][0], F.v[slot][1], F.v[slot][2], F.v[slot][3], F.v[slot][4]};
+            __syncthreads();
+        }
+        if (recv) v = fe_carry(fe_add(fe_mul(v, mP), w));
+        if (2 * L < N) mP = mk_mul(fe_mul(mul_fe(mP), mP)); /* r^(2L) */
+    }
+    /* thread 0: the tag; every lane of the group got the same tree, so
+       only thread 0's value is the sum */
+    if (t == 0) {
+        v = fe_mul(v, mk_mul(r));
+        const uint32_t s[4] = {F.rs[4], F.rs[5], F.rs[6], F.rs[7]};
+        uint32_t tag[4];
+        fe_finish(v, s, tag);
+        if (OPEN) {
+            uint32_t got[4];
+            load16(rec + len, 16, got);
+            F.verdict = tag_equal(tag, got) ? 1u : 0u;
+        } else {
+            store16(rec + len, 16, tag);
+        }
+    }
+    if (!OPEN) return true;
+    __syncthreads();
+    const bool ok = F.verdict != 0;
+    if (ok && q >= 1 && q <= J) {
+        uint32_t *w = (uint32_t *)(rec + 64 * (q - 1) + 4 * c);
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) w[4 * i2] = pt[i2]; /* bytes past len: not copied out */
+    }
+    return ok;
+}
+
 /* One 16-byte system-coherent load (a single request: the chunk is read
    whole, never half before and half after the host's 16-byte store). */
 NA_DEV uint4 load_sys16(const uint32_t *p)
@@ -130,6 +299,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
     __shared__ uint32_t cgen[WORKER_CTX_SLOTS], cuse[WORKER_CTX_SLOTS];
     __shared__ uint32_t hdr[16];
     __shared__ uint32_t verdict, s_cmd; /* s_cmd: 0 wait, 1 serve, 2 leave */
+    __shared__ FastLds fast;
     __shared__ __attribute__((aligned(16))) uint8_t buf[WORKER_DATA];
     const uint32_t t = threadIdx.x;
     aes_table_entry(t, sb[t], te[t]);
@@ -215,7 +385,10 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
         const uint64_t c_in = __builtin_amdgcn_s_memtime();
         uint8_t *key = buf, *ad = buf + 32, *rec = buf + 32 + ad_pad;
         bool ok = true;
-        if (cipher == NOISE_CIPHER_CHACHAPOLY) {
+        if (cipher == NOISE_CIPHER_CHACHAPOLY && worker_fast_fits(len, ad_len)) {
+            ok = op ? worker_chacha_fast<true>(rec, ad, ad_len, len, key, nonce, fast)
+                    : worker_chacha_fast<false>(rec, ad, ad_len, len, key, nonce, fast);
+        } else if (cipher == NOISE_CIPHER_CHACHAPOLY) {
             RecView rv;
             rv.src = rec;
             rv.dst = rec;
@@ -273,8 +446,9 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
         }
         last = seq;
         quiet = __builtin_amdgcn_s_memrealtime();
-        /* scrub this record's bytes (and the key) from LDS before the next one */
-        for (uint32_t o = 16 * t; o < bytes; o += 16 * 256) *(uint4 *)(buf + o) = make_uint4(0, 0, 0, 0);
+        /* scrub this record's bytes (and the key) from LDS before the next one;
+           the kernels may have written whole 64-B units past len + 16 */
+        for (uint32_t o = 16 * t; o < bytes + 64; o += 16 * 256) *(uint4 *)(buf + o) = make_uint4(0, 0, 0, 0);
         __syncthreads();
     }
     /* the cached AES-GCM contexts hold key material too */
