@@ -275,7 +275,10 @@ def kernel_name(cipher, n, rps, lanes, in_stride, out_stride, length, duplex=Fal
     if cipher == AES:
         c = "true" if ct else "false"
         if fast and rps % 256 == 0:
-            return f"gcm_duplex_staged<{c}>" if duplex else f"gcm_staged<false, {c}>"
+            if duplex:  # launch_aes.hip aes_duplex: the fused kernel unless told otherwise
+                staged = os.environ.get("NOISE_AEAD_GCM_DUPLEX") == "staged"
+                return f"gcm_duplex_{'staged' if staged else 'fused'}<{c}>"
+            return f"gcm_staged<false, {c}>"
         return f"gcm_uniform<false, {c}>"
     if fast and lanes >= 4:
         return f"chachapoly_seal_staged<{lanes}, {'true' if rps % (64 // lanes) == 0 else 'false'}>"

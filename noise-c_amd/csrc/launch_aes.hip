@@ -122,12 +122,15 @@ int aes_uniform(const UniformArgs &a, bool open, bool ct, bool staged, hipStream
     return hip_rc(hipGetLastError());
 }
 
-/* NOISE_AEAD_GCM_DUPLEX=fused | staged selects the duplex kernel (A/B runs) */
+/* The fused duplex kernel (one LDS fill, seal then open per workgroup) by
+   default: C3 +0.7-0.9 % in three interleaved rounds
+   (profiles/r03/gcm_fused_ab.jsonl); NOISE_AEAD_GCM_DUPLEX=staged selects
+   gcm_duplex_staged (A/B runs). */
 static bool gcm_duplex_fused_on()
 {
     static const bool v = [] {
         const char *e = getenv("NOISE_AEAD_GCM_DUPLEX");
-        return e && !strcmp(e, "fused");
+        return !(e && !strcmp(e, "staged"));
     }();
     return v;
 }

@@ -56,6 +56,19 @@ constexpr uint32_t WORKER_MAX_LEN = 65535 - 16; /* whole records only */
 constexpr uint32_t WORKER_MAX_AD = 256;
 /* data area: ChaCha key (32 B) || AD (padded to 16) || record || tag */
 constexpr uint32_t WORKER_DATA = 32 + WORKER_MAX_AD + 65536 + 64;
+/* The request's input stream (key || AD padded to 16 || record || tag) is
+   posted as 16-byte chunks of 12 stream bytes and the request's sequence
+   number, each written with one 16-byte store: a chunk carries its own
+   proof of freshness.  So the worker can read the first WORKER_SPEC chunks
+   speculatively with every poll of the header (4 KiB per poll, one PCIe
+   round trip for header and data together) and keep the ones stamped with
+   the new number, re-reading only stale ones. */
+constexpr uint32_t WCHUNK_BYTES = 12;
+constexpr uint32_t WORKER_SPEC = 256; /* chunks read with every poll: one per thread */
+constexpr uint32_t WORKER_HEAD = WORKER_SPEC * WCHUNK_BYTES; /* stream bytes sent as chunks */
+/* the stream past the head (records over ~3 KiB) is posted raw, read after the header */
+constexpr uint32_t WORKER_TAIL = WORKER_DATA - WORKER_HEAD;
+static_assert(WORKER_HEAD % 16 == 0, "the raw tail lands 16-B aligned in LDS");
 /* AES-GCM contexts the worker keeps in LDS (an echo session uses two) */
 constexpr int WORKER_CTX_SLOTS = 2;
 constexpr uint32_t WORKER_CTX_BYTES = offsetof(AesCtx, tab8); /* rk, H, H^1..H^4 */
@@ -75,7 +88,7 @@ struct alignas(128) WorkerSlot {
     uint8_t pad0[128 - 64];
     /* worker -> host */
     uint64_t done;     /* last request completed */
-    uint32_t status;   /* 0 ok, 1 MAC failure */
+    uint32_t status;   /* 0 ok, 1 MAC failure, 2 input never arrived */
     uint32_t exiting;  /* the worker is leaving (or has left) */
     uint32_t stamps[8]; /* debug: s_memrealtime (10 ns) of the last request's phases */
     uint8_t pad1[128 - 48];
@@ -286,12 +299,22 @@ NA_DEV uint4 load_sys16(const uint32_t *p)
     return v;
 }
 
+/* two system-coherent 16-byte loads in one round trip */
+NA_DEV void load_sys16x2(const uint32_t *p, const uint32_t *q, uint4 &a, uint4 &b)
+{
+    asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+                 "global_load_dwordx4 %1, %3, off sc0 sc1\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=&v"(a), "=&v"(b) : "v"(p), "v"(q) : "memory");
+}
+
 NA_DEV uint32_t now10ns() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
 
 /* 256 threads.  last: the last request already served; idle/lifetime in
    s_memrealtime ticks (100 MHz). */
-__global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *data, uint32_t last,
-                                                   uint64_t idle, uint64_t lifetime)
+__global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint4 *in, const uint8_t *tail,
+                                                   uint8_t *out, uint32_t last, uint64_t idle,
+                                                   uint64_t lifetime)
 {
     __shared__ uint32_t te[256], sb[256];
     __shared__ __attribute__((aligned(16))) uint8_t cbuf[WORKER_CTX_SLOTS][WORKER_CTX_BYTES];
@@ -299,6 +322,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
     __shared__ uint32_t cgen[WORKER_CTX_SLOTS], cuse[WORKER_CTX_SLOTS];
     __shared__ uint32_t hdr[16];
     __shared__ uint32_t verdict, s_cmd; /* s_cmd: 0 wait, 1 serve, 2 leave */
+    __shared__ uint32_t s_stale;        /* chunks still stamped with an older request */
     __shared__ FastLds fast;
     __shared__ __attribute__((aligned(16))) uint8_t buf[WORKER_DATA];
     const uint32_t t = threadIdx.x;
@@ -314,9 +338,12 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
     uint32_t tick = 0;
     for (;;) {
         uint32_t t_seen = 0;
-        if (t < 64) { /* wave 0 polls: lanes 0..3 read one header chunk each */
-            uint4 c = make_uint4(0, 0, 0, 0);
-            if (t < 4) c = load_sys16(slot->c0 + 4 * t);
+        /* every thread reads input chunk t; wave 0's lanes 0..3 hold the
+           header (other lanes read a header chunk too: same round trip) */
+        uint4 c, mine;
+        load_sys16x2(slot->c0 + 4 * (t & 3), (const uint32_t *)(in + t), c, mine);
+        if (t == 0) s_stale = 0;
+        if (t < 64) {
             const uint32_t s0 = __shfl((int)c.x, 0, 64), s1 = __shfl((int)c.x, 1, 64);
             const uint32_t s2 = __shfl((int)c.x, 2, 64), s3 = __shfl((int)c.x, 3, 64);
             const uint32_t stop = __shfl((int)c.w, 2, 64);
@@ -363,8 +390,21 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
         const uint32_t ad_pad = (ad_len + 15) & ~15u;
         const uint32_t bytes = 32 + ad_pad + len + 16;
         const uint32_t t_fence = now10ns();
-        for (uint32_t o = 16 * t; o < bytes; o += 16 * 256)
-            *(uint4 *)(buf + o) = *(const uint4 *)(data + o);
+        /* the input stream: the head as stamped chunks (chunk t read
+           speculatively with the poll, re-read while stale), the rest raw
+           (written before the header, read after it) */
+        const uint32_t total = 32 + ad_pad + len + (op ? 16u : 0u);
+        const uint32_t nchunks = min((total + WCHUNK_BYTES - 1) / WCHUNK_BYTES, WORKER_SPEC);
+        if (t < nchunks) {
+            uint4 v = mine;
+            for (uint32_t tries = 0; v.w != seq && tries < (1u << 20); ++tries)
+                v = load_sys16((const uint32_t *)(in + t));
+            if (v.w != seq) s_stale = 1; /* never in practice: the host wrote it before the header */
+            uint32_t *d = (uint32_t *)(buf + WCHUNK_BYTES * t);
+            d[0] = v.x; d[1] = v.y; d[2] = v.z;
+        }
+        for (uint32_t o = 16 * t; WORKER_HEAD + o < total; o += 16 * 256)
+            *(uint4 *)(buf + WORKER_HEAD + o) = *(const uint4 *)(tail + o);
         int cs = 0;
         if (cipher == NOISE_CIPHER_AESGCM) { /* the context: cached, or copied into the LRU slot */
             cs = ctag[0] == ctx_addr && cgen[0] == gen ? 0 : (ctag[1] == ctx_addr && cgen[1] == gen ? 1 : -1);
@@ -424,15 +464,16 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, uint8_t *da
         /* results back: seal CT || tag, open the plaintext (only if verified);
            every storing wave drains its stores, then one system release and
            the flag (MI355X_MICROARCH.md, inter-workgroup visibility) */
-        const uint32_t out = op ? (ok ? len : 0u) : len + 16;
-        uint8_t *dout = data + 32 + ad_pad;
-        for (uint32_t o = 16 * t; o < ((out + 15) & ~15u); o += 16 * 256)
-            *(uint4 *)(dout + o) = *(const uint4 *)(rec + o);
+        const bool stale = s_stale != 0;
+        if (stale) ok = false;
+        const uint32_t nout = op ? (ok ? len : 0u) : (stale ? 0u : len + 16);
+        for (uint32_t o = 16 * t; o < ((nout + 15) & ~15u); o += 16 * 256)
+            *(uint4 *)(out + o) = *(const uint4 *)(rec + o);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0) {
             const uint32_t t_out = now10ns();
-            slot->status = ok ? 0u : 1u;
+            slot->status = stale ? 2u : (ok ? 0u : 1u);
             slot->stamps[0] = t_seen;
             slot->stamps[1] = t_fence;
             slot->stamps[2] = t_in;
@@ -465,7 +506,9 @@ struct Worker {
     int state = 0;             /* 0 unknown, 1 usable, -1 disabled */
     WorkerSlot *slot = nullptr; /* host view */
     WorkerSlot *dslot = nullptr; /* device view */
-    uint8_t *data = nullptr, *ddata = nullptr;
+    uint4 *in = nullptr, *din = nullptr;       /* the stream's head: stamped chunks */
+    uint8_t *tail = nullptr, *dtail = nullptr; /* the rest of the stream, raw */
+    uint8_t *out = nullptr, *dout = nullptr;   /* raw results */
     hipStream_t stream = nullptr;
     uint32_t seq = 0;
     bool launched = false;
@@ -503,13 +546,18 @@ int worker_setup(Worker &w)
 {
     if (w.state) return w.state;
     w.state = -1;
-    if (hipHostMalloc((void **)&w.slot, sizeof(WorkerSlot) + WORKER_DATA,
-                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    const size_t in_bytes = (size_t)WORKER_SPEC * 16, tail_bytes = WORKER_TAIL + 64;
+    const size_t total = sizeof(WorkerSlot) + in_bytes + tail_bytes + WORKER_DATA;
+    if (hipHostMalloc((void **)&w.slot, total, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         return -1;
-    memset(w.slot, 0, sizeof(WorkerSlot) + WORKER_DATA);
+    memset(w.slot, 0, total); /* chunk stamps 0: no request has that number */
     if (hipHostGetDevicePointer((void **)&w.dslot, w.slot, 0) != hipSuccess) return -1;
-    w.data = (uint8_t *)(w.slot + 1);
-    w.ddata = (uint8_t *)(w.dslot + 1);
+    w.in = (uint4 *)(w.slot + 1);
+    w.din = (uint4 *)(w.dslot + 1);
+    w.tail = (uint8_t *)(w.in + WORKER_SPEC);
+    w.dtail = (uint8_t *)(w.din + WORKER_SPEC);
+    w.out = w.tail + tail_bytes;
+    w.dout = w.dtail + tail_bytes;
     if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess) return -1;
     std::call_once(g_atexit_once, [] { atexit(worker_stop_all); });
     w.state = 1;
@@ -521,8 +569,8 @@ int worker_launch(Worker &w)
     (void)hipStreamSynchronize(w.stream); /* a previous worker has left */
     __atomic_store_n(&w.slot->exiting, 0u, __ATOMIC_RELEASE);
     __atomic_store_n(&w.slot->c2[3], 0u, __ATOMIC_RELEASE); /* stop */
-    hipLaunchKernelGGL(aead_worker, dim3(1), dim3(256), 0, w.stream, w.dslot, w.ddata,
-                       w.seq, IDLE_TICKS, LIFETIME_TICKS);
+    hipLaunchKernelGGL(aead_worker, dim3(1), dim3(256), 0, w.stream, w.dslot, (const uint4 *)w.din,
+                       (const uint8_t *)w.dtail, w.dout, w.seq, IDLE_TICKS, LIFETIME_TICKS);
     if (hipGetLastError() != hipSuccess) return NOISE_ERROR_SYSTEM;
     w.launched = true;
     return NOISE_ERROR_NONE;
@@ -576,15 +624,30 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     if (h_ctx && hipHostGetDevicePointer(&d_hctx, (void *)h_ctx, 0) != hipSuccess)
         return NOISE_ERROR_NOT_APPLICABLE;
     const size_t ad_pad = (ad_len + 15) & ~(size_t)15;
-    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) memcpy(w.data, key, 32);
-    if (ad_len) memcpy(w.data + 32, ad, ad_len);
-    memcpy(w.data + 32 + ad_pad, data, len + (open ? 16 : 0));
     WorkerSlot *s = w.slot;
     if (!w.launched || __atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE)) {
         const int rc = worker_launch(w);
         if (rc) return rc;
     }
     const uint32_t k = ++w.seq;
+    /* the input stream key || AD || pad || record (|| tag): its first
+       WORKER_HEAD bytes as stamped chunks (12 stream bytes + k), the rest raw */
+    const size_t in_len = len + (open ? 16 : 0), total = 32 + ad_pad + in_len;
+    const size_t head = total < WORKER_HEAD ? total : WORKER_HEAD;
+    const size_t nchunks = (head + WCHUNK_BYTES - 1) / WCHUNK_BYTES;
+    alignas(16) uint8_t tmp[WORKER_HEAD + 16];
+    memset(tmp, 0, 32 + ad_pad);
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) memcpy(tmp, key, 32);
+    if (ad_len) memcpy(tmp + 32, ad, ad_len);
+    memcpy(tmp + 32 + ad_pad, data, head - 32 - ad_pad);
+    memset(tmp + head, 0, 16); /* the last chunk's bytes past the stream */
+    const __m128i keep = _mm_set_epi32(0, -1, -1, -1), stamp = _mm_set_epi32((int)k, 0, 0, 0);
+    for (size_t c = 0; c < nchunks; ++c) {
+        const __m128i v = _mm_loadu_si128((const __m128i *)(tmp + WCHUNK_BYTES * c));
+        _mm_store_si128((__m128i *)(w.in + c), _mm_or_si128(_mm_and_si128(v, keep), stamp));
+    }
+    explicit_bzero(tmp, head);
+    if (total > head) memcpy(w.tail, data + (head - 32 - ad_pad), total - head);
     const uint64_t ctx = (uint64_t)(uintptr_t)d_hctx;
     __atomic_thread_fence(__ATOMIC_RELEASE); /* the data area before the header */
     store_chunk(s->c0, k, (open ? 1u : 0u) | (ct_env() ? 1u << 8 : 0u), (uint32_t)len, (uint32_t)ad_len);
@@ -606,11 +669,14 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
         }
         if (spins > (1ull << 32)) return NOISE_ERROR_SYSTEM; /* never in practice */
     }
-    const int st = s->status ? NOISE_ERROR_MAC_FAILURE : NOISE_ERROR_NONE;
-    uint8_t *res = w.data + 32 + ad_pad;
-    if (!open) memcpy(data, res, len + 16);
-    else if (st == NOISE_ERROR_NONE) memcpy(data, res, len);
-    explicit_bzero(w.data, 32 + ad_pad + len + 16);
+    const uint32_t status = s->status;
+    const int st = status == 2 ? NOISE_ERROR_SYSTEM : (status ? NOISE_ERROR_MAC_FAILURE : NOISE_ERROR_NONE);
+    if (st == NOISE_ERROR_NONE) memcpy(data, w.out, open ? len : len + 16);
+    /* key, plaintext and results out of the shared host memory; the stamps
+       stay (a zeroed chunk would carry number 0, which no request has) */
+    for (size_t c = 0; c < nchunks; ++c) _mm_store_si128((__m128i *)(w.in + c), stamp);
+    if (total > head) explicit_bzero(w.tail, total - head);
+    explicit_bzero(w.out, len + 16);
     return st;
 }
 

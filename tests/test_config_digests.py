@@ -147,7 +147,7 @@ def test_full_size_duplex_at_bench_slots(name):
     """The kernels bench.py times: C2 / C3 at full size
     through noise_aead_dev_duplex_uniform at the bench's 128-B record slots
     (in_stride 1408, out_stride 1536), one state, recs_per_state 65 536 —
-    chachapoly_duplex_staged<4, true> / gcm_duplex_staged<false>.  The seal
+    chachapoly_duplex_staged<4, true> / gcm_duplex_fused<false>.  The seal
     half's sealed records hash to the golden digest (cipher-chachapoly.c
     :107-133 / cipher-aesgcm.c:156-170 bytes); the open half, over a batch
     sealed beforehand with 64 records tampered, accepts every other record

@@ -248,7 +248,7 @@ def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout, flags):
     nonces, length, record count; some records tampered) in one call must
     equal the two separate calls — i.e. the oracle — byte for byte.  ChaCha
     FAST layouts run the one-launch chachapoly_duplex_staged kernel; AES-GCM
-    with one state per 256 records runs gcm_duplex_staged (plain and CT
+    with one state per 256 records runs gcm_duplex_fused (plain and CT
     GHASH); the others, and a VERIFY_FIRST open, two launches.  A rejected
     record's output is zeroed (one-pass opens) or never written
     (VERIFY_FIRST)."""

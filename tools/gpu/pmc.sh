@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/$name -o run --output-format csv -- \
-      python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 10 --warmup 2 $EXTRA > $OUT/$name.log 2>&1
+      python3 $R/bench.py --config $CFG --no-cpu-baseline --no-verify --settle-ms 0 --steps 10 --warmup 2 $EXTRA > $OUT/$name.log 2>&1
   echo "pmc $name rc=$?"
 }
 run fetch FETCH_SIZE || exit 1
