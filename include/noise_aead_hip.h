@@ -388,6 +388,9 @@ void noise_aead_debug_worker_stamps(uint32_t *out, int n);
 /* noise_aead_debug_worker_clock_mhz: the shader clock of that request's
  *   compute phase (s_memtime cycles / s_memrealtime time), 0 if none. */
 double noise_aead_debug_worker_clock_mhz(void);
+/* noise_aead_debug_worker_fast_stamps: shader-cycle stamps through the
+ *   worker's latency-first ChaChaPoly path (n <= 8). */
+void noise_aead_debug_worker_fast_stamps(uint32_t *out, int n);
 void *noise_aead_debug_last_freed_ctx(size_t *bytes);
 
 /* Default lanes per record the library picks for a batch of n records. */

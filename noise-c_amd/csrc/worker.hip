@@ -91,7 +91,8 @@ struct alignas(128) WorkerSlot {
     uint32_t status;   /* 0 ok, 1 MAC failure, 2 input never arrived */
     uint32_t exiting;  /* the worker is leaving (or has left) */
     uint32_t stamps[8]; /* debug: s_memrealtime (10 ns) of the last request's phases */
-    uint8_t pad1[128 - 48];
+    uint32_t fstamps[8]; /* debug: s_memtime (cycles) through the latency-first path */
+    uint8_t pad1[128 - 80];
 };
 static_assert(sizeof(WorkerSlot) == 256, "slot layout");
 
@@ -187,6 +188,7 @@ NA_DEV void lds_block(const uint8_t *p, uint32_t n, uint32_t w[4])
 }
 
 struct FastLds {
+    uint32_t dbg[8];         /* s_memtime stamps of thread 0 (debug hook) */
     uint32_t rs[8];          /* r, s (key stream words 0..7 of block 0) */
     uint32_t v[4][5];        /* the tree's cross-wave partners (levels 64, 128) */
     uint32_t verdict;
@@ -200,6 +202,8 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
 {
     const int t = (int)threadIdx.x, lane = t & 63, c = t & 3;
     const uint32_t q = (uint32_t)t >> 2; /* ChaCha block */
+    const uint64_t c00 = __builtin_amdgcn_s_memtime();
+#define NA_FSTAMP(k) do { if (t == 0) F.dbg[k] = (uint32_t)(__builtin_amdgcn_s_memtime() - c00); } while (0)
     uint32_t key[8];
     load_key(key8, key);
     const uint32_t n_lo = (uint32_t)nonce, n_hi = (uint32_t)(nonce >> 32);
@@ -207,6 +211,7 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
     uint32_t ks[4] = {0, 0, 0, 0};
     if (q <= J) chacha_quad(key, q, n_lo, n_hi, c, ks[0], ks[1], ks[2], ks[3]);
     if (q == 0) { F.rs[c] = ks[0]; F.rs[4 + c] = ks[1]; }
+    NA_FSTAMP(0); /* ChaCha done (thread 0's quad) */
     /* data words 64(q-1) + 4c + 16i, i = 0..3: key stream word 4i + c */
     uint32_t pt[4] = {0, 0, 0, 0};
     if (q >= 1 && q <= J) {
@@ -218,6 +223,7 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
         }
     }
     __syncthreads();
+    NA_FSTAMP(1); /* CT in LDS, r and s published */
     /* Poly1305 block of this lane, right-justified in N lanes */
     const uint32_t a = (ad_len + 15) / 16, m = (len + 15) / 16, n = a + m + 1;
     const uint32_t N = n <= 1 ? 1u : 1u << (32 - __builtin_clz(n - 1));
@@ -237,6 +243,7 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
     }
     const Fe r = fe_clamp_r(F.rs[0], F.rs[1], F.rs[2], F.rs[3]);
     Mul mP = mk_mul(r); /* r^L */
+    NA_FSTAMP(2); /* Poly block loaded */
 #pragma unroll 1 /* barriers inside: hipcc does not unroll it */
     for (uint32_t L = 1; L < 256; L <<= 1) {
         if (L >= N) break; /* uniform */
@@ -263,6 +270,7 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
         if (recv) v = fe_carry(fe_add(fe_mul(v, mP), w));
         if (2 * L < N) mP = mk_mul(fe_mul(mul_fe(mP), mP)); /* r^(2L) */
     }
+    NA_FSTAMP(3); /* tree done */
     /* thread 0: the tag; every lane of the group got the same tree, so
        only thread 0's value is the sum */
     if (t == 0) {
@@ -278,6 +286,7 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
             store16(rec + len, 16, tag);
         }
     }
+    NA_FSTAMP(4); /* tag */
     if (!OPEN) return true;
     __syncthreads();
     const bool ok = F.verdict != 0;
@@ -286,6 +295,8 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
 #pragma unroll
         for (int i2 = 0; i2 < 4; ++i2) w[4 * i2] = pt[i2]; /* bytes past len: not copied out */
     }
+    NA_FSTAMP(5);
+#undef NA_FSTAMP
     return ok;
 }
 
@@ -480,6 +491,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint4
             slot->stamps[3] = t_done;
             slot->stamps[4] = t_out;
             slot->stamps[6] = c_run;
+            for (int k = 0; k < 8; ++k) slot->fstamps[k] = fast.dbg[k];
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             slot->stamps[5] = now10ns();
@@ -690,6 +702,16 @@ extern "C" void noise_aead_debug_worker_stamps(uint32_t *out, int n)
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
     const WorkerSlot *s = g_worker[dev].slot;
     for (int i = 0; i < n && i < 5; ++i) out[i] = s ? s->stamps[i + 1] - s->stamps[0] : 0;
+}
+
+/* Test hook: the latency-first path's s_memtime stamps (cycles from its
+   start: ChaCha, CT in LDS, Poly blocks loaded, tree, tag, open's write). */
+extern "C" void noise_aead_debug_worker_fast_stamps(uint32_t *out, int n)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
+    const WorkerSlot *s = g_worker[dev].slot;
+    for (int i = 0; i < n && i < 8; ++i) out[i] = s ? s->fstamps[i] : 0;
 }
 
 /* Test hook: the shader clock (MHz) of the last worker request's compute

@@ -43,6 +43,7 @@ int main(int argc, char **argv)
     double *te = malloc(iters * sizeof(double)), *td = malloc(iters * sizeof(double));
     double ph[5] = {0, 0, 0, 0, 0}; /* resident-worker phase stamps (us), decrypt calls */
     double mhz = 0;                 /* the worker's shader clock while computing */
+    double fs[6] = {0, 0, 0, 0, 0, 0}; /* latency-first path stamps (cycles), decrypt calls */
     int ok = 1;
     for (int it = -50; it < iters; ++it) { /* 50 untimed warm-up messages */
         NoiseBuffer b;
@@ -61,6 +62,9 @@ int main(int argc, char **argv)
             noise_aead_debug_worker_stamps(st, 5);
             for (int i = 0; i < 5; ++i) ph[i] += st[i] * 0.01 / iters;
             mhz += noise_aead_debug_worker_clock_mhz() / iters;
+            uint32_t f[6];
+            noise_aead_debug_worker_fast_stamps(f, 6);
+            for (int i = 0; i < 6; ++i) fs[i] += (double)f[i] / iters;
         }
     }
     qsort(te, iters, sizeof(double), cmp_d);
@@ -69,9 +73,12 @@ int main(int argc, char **argv)
            "\"encrypt_us_p50\": %.2f, \"encrypt_us_p99\": %.2f, "
            "\"decrypt_us_p50\": %.2f, \"decrypt_us_p99\": %.2f, "
            "\"worker_phase_us\": {\"fence\": %.2f, \"inputs\": %.2f, \"computed\": %.2f, "
-           "\"written\": %.2f, \"released\": %.2f}, \"worker_clock_mhz\": %.0f, \"ok\": %s}\n",
+           "\"written\": %.2f, \"released\": %.2f}, \"worker_clock_mhz\": %.0f, "
+           "\"fast_path_cycles\": {\"chacha\": %.0f, \"ct_in_lds\": %.0f, \"poly_loaded\": %.0f, "
+           "\"tree\": %.0f, \"tag\": %.0f, \"plaintext\": %.0f}, \"ok\": %s}\n",
            name, len, iters, te[iters / 2], te[iters * 99 / 100], td[iters / 2],
-           td[iters * 99 / 100], ph[0], ph[1], ph[2], ph[3], ph[4], mhz, ok ? "true" : "false");
+           td[iters * 99 / 100], ph[0], ph[1], ph[2], ph[3], ph[4], mhz, fs[0], fs[1], fs[2], fs[3], fs[4], fs[5],
+           ok ? "true" : "false");
     noise_cipherstate_free(tx);
     noise_cipherstate_free(rx);
     return ok ? 0 : 1;
