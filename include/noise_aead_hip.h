@@ -391,6 +391,9 @@ double noise_aead_debug_worker_clock_mhz(void);
 /* noise_aead_debug_worker_fast_stamps: shader-cycle stamps through the
  *   worker's latency-first ChaChaPoly path (n <= 8). */
 void noise_aead_debug_worker_fast_stamps(uint32_t *out, int n);
+/* noise_aead_debug_worker_host_ns: the calling thread's last worker call on
+ *   the host, ns from its start: packed, doorbell, done seen, returned. */
+void noise_aead_debug_worker_host_ns(uint64_t *out, int n);
 void *noise_aead_debug_last_freed_ctx(size_t *bytes);
 
 /* Default lanes per record the library picks for a batch of n records. */

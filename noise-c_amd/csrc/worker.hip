@@ -49,6 +49,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <ctime>
 
 namespace na {
 
@@ -194,13 +195,56 @@ struct FastLds {
     uint32_t verdict;
 };
 
+/* v of lane t + L (the tree's partner) for L < 64: DPP where the partner is
+   in the same row of 16 lanes, a lane shuffle otherwise */
+template <uint32_t L>
+NA_DEV uint32_t from_plus(uint32_t x, int lane)
+{
+    if constexpr (L == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xb1, 0xf, 0xf, false);  /* quad [1,0,3,2] */
+    else if constexpr (L == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4e, 0xf, 0xf, false); /* quad [2,3,0,1] */
+    else if constexpr (L == 4) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xf, 0xf, false); /* row_shl:4 */
+    else if constexpr (L == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x108, 0xf, 0xf, false); /* row_shl:8 */
+    else return (uint32_t)__shfl((int)x, lane + (int)L, 64);
+}
+
+/* One level of the Poly1305 tree: lanes j = 0 mod 2L set v_j = v_j r^L + v_{j+L};
+   mP holds r^L on entry and r^(2L) on exit (when a next level exists). */
+template <uint32_t L>
+NA_DEV void tree_level(Fe &v, Mul &mP, int t, uint32_t N, FastLds &F)
+{
+    if (L >= N) return; /* uniform */
+    const int lane = t & 63;
+    Fe w;
+    if constexpr (L < 64) {
+        w.l0 = from_plus<L>(v.l0, lane);
+        w.l1 = from_plus<L>(v.l1, lane);
+        w.l2 = from_plus<L>(v.l2, lane);
+        w.l3 = from_plus<L>(v.l3, lane);
+        w.l4 = from_plus<L>(v.l4, lane);
+    } else {
+        /* partner t + L sits in another wave: through LDS */
+        if (lane == 0 && (t & (int)(2 * L - 1)) == (int)L) {
+            const int slot = t >> 6;
+            F.v[slot][0] = v.l0; F.v[slot][1] = v.l1; F.v[slot][2] = v.l2;
+            F.v[slot][3] = v.l3; F.v[slot][4] = v.l4;
+        }
+        __syncthreads();
+        const int slot = min((t + (int)L) >> 6, 3); /* receivers: 1, 2 or 3 */
+        w = Fe{F.v[slot][0], F.v[slot][1], F.v[slot][2], F.v[slot][3], F.v[slot][4]};
+        __syncthreads();
+    }
+    const Mul cur = mP;
+    if (2 * L < N) mP = mk_mul(fe_mul(mul_fe(cur), cur)); /* r^(2L), off the chain */
+    if ((t & (int)(2 * L - 1)) == 0) v = fe_carry(fe_add(fe_mul(v, cur), w));
+}
+
 /* rec: len bytes (+ the tag for open) in LDS, 16-B aligned; ad: ad_len bytes
    (16-B aligned, padded).  256 threads, every one calls this. */
 template <bool OPEN>
 NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len, uint32_t len,
                                const uint8_t *key8, uint64_t nonce, FastLds &F)
 {
-    const int t = (int)threadIdx.x, lane = t & 63, c = t & 3;
+    const int t = (int)threadIdx.x, c = t & 3;
     const uint32_t q = (uint32_t)t >> 2; /* ChaCha block */
     const uint64_t c00 = __builtin_amdgcn_s_memtime();
 #define NA_FSTAMP(k) do { if (t == 0) F.dbg[k] = (uint32_t)(__builtin_amdgcn_s_memtime() - c00); } while (0)
@@ -244,32 +288,16 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
     const Fe r = fe_clamp_r(F.rs[0], F.rs[1], F.rs[2], F.rs[3]);
     Mul mP = mk_mul(r); /* r^L */
     NA_FSTAMP(2); /* Poly block loaded */
-#pragma unroll 1 /* barriers inside: hipcc does not unroll it */
-    for (uint32_t L = 1; L < 256; L <<= 1) {
-        if (L >= N) break; /* uniform */
-        const bool recv = (t & (2 * L - 1)) == 0;
-        Fe w;
-        if (L < 64) {
-            w.l0 = (uint32_t)__shfl((int)v.l0, lane + (int)L, 64);
-            w.l1 = (uint32_t)__shfl((int)v.l1, lane + (int)L, 64);
-            w.l2 = (uint32_t)__shfl((int)v.l2, lane + (int)L, 64);
-            w.l3 = (uint32_t)__shfl((int)v.l3, lane + (int)L, 64);
-            w.l4 = (uint32_t)__shfl((int)v.l4, lane + (int)L, 64);
-        } else {
-            /* partner t + L sits in another wave: through LDS */
-            if (lane == 0 && (t & (int)(2 * L - 1)) == (int)L) {
-                const int slot = t >> 6;
-                F.v[slot][0] = v.l0; F.v[slot][1] = v.l1; F.v[slot][2] = v.l2;
-                F.v[slot][3] = v.l3; F.v[slot][4] = v.l4;
-            }
-            __syncthreads();
-            const int slot = min((t + (int)L) >> 6, 3); /* receivers: 1, 2 or 3 */
-            w = Fe{F.v[slot][0], F.v[slot][1], F.v[slot][2], F.v[slot][3], F.v[slot][4]};
-            __syncthreads();
-        }
-        if (recv) v = fe_carry(fe_add(fe_mul(v, mP), w));
-        if (2 * L < N) mP = mk_mul(fe_mul(mul_fe(mP), mP)); /* r^(2L) */
-    }
+    /* levels 1..8 by DPP (quad swaps, row shifts), 16 and 32 by lane
+       shuffles, 64 and 128 through LDS; each level a uniform branch on N */
+    tree_level<1>(v, mP, t, N, F);
+    tree_level<2>(v, mP, t, N, F);
+    tree_level<4>(v, mP, t, N, F);
+    tree_level<8>(v, mP, t, N, F);
+    tree_level<16>(v, mP, t, N, F);
+    tree_level<32>(v, mP, t, N, F);
+    tree_level<64>(v, mP, t, N, F);
+    tree_level<128>(v, mP, t, N, F);
     NA_FSTAMP(3); /* tree done */
     /* thread 0: the tag; every lane of the group got the same tree, so
        only thread 0's value is the sum */
@@ -620,10 +648,21 @@ static inline void store_chunk(uint32_t *dst, uint32_t a, uint32_t b, uint32_t c
    state's context and the generation it was written at.  Returns
    NOISE_ERROR_NONE, _MAC_FAILURE, _SYSTEM, or _NOT_APPLICABLE (take the
    launch path). */
+/* host-side phase times of the last request (ns, CLOCK_MONOTONIC): packed,
+   doorbell written, done seen, returned — relative to the call's start */
+static thread_local uint64_t t_host[4];
+static inline uint64_t host_ns()
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, const void *h_ctx,
                                          uint32_t gen, uint64_t nonce, const uint8_t *ad,
                                          size_t ad_len, uint8_t *data, size_t len, int open)
 {
+    const uint64_t h0 = host_ns();
     if (cipher_id == NOISE_CIPHER_AESGCM && !h_ctx) return NOISE_ERROR_NOT_APPLICABLE;
     if (!worker_enabled() || len > WORKER_MAX_LEN || ad_len > WORKER_MAX_AD)
         return NOISE_ERROR_NOT_APPLICABLE;
@@ -661,11 +700,13 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     explicit_bzero(tmp, head);
     if (total > head) memcpy(w.tail, data + (head - 32 - ad_pad), total - head);
     const uint64_t ctx = (uint64_t)(uintptr_t)d_hctx;
+    const uint64_t h1 = host_ns();
     __atomic_thread_fence(__ATOMIC_RELEASE); /* the data area before the header */
     store_chunk(s->c0, k, (open ? 1u : 0u) | (ct_env() ? 1u << 8 : 0u), (uint32_t)len, (uint32_t)ad_len);
     store_chunk(s->c1, k, (uint32_t)nonce, (uint32_t)(nonce >> 32), (uint32_t)cipher_id);
     store_chunk(s->c2, k, (uint32_t)ctx, (uint32_t)(ctx >> 32), 0u);
     store_chunk(s->c3, k, gen, 0u, 0u);
+    const uint64_t h2 = host_ns();
     uint64_t spins = 0;
     while (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
         __builtin_ia32_pause();
@@ -681,6 +722,7 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
         }
         if (spins > (1ull << 32)) return NOISE_ERROR_SYSTEM; /* never in practice */
     }
+    const uint64_t h3 = host_ns();
     const uint32_t status = s->status;
     const int st = status == 2 ? NOISE_ERROR_SYSTEM : (status ? NOISE_ERROR_MAC_FAILURE : NOISE_ERROR_NONE);
     if (st == NOISE_ERROR_NONE) memcpy(data, w.out, open ? len : len + 16);
@@ -689,6 +731,8 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     for (size_t c = 0; c < nchunks; ++c) _mm_store_si128((__m128i *)(w.in + c), stamp);
     if (total > head) explicit_bzero(w.tail, total - head);
     explicit_bzero(w.out, len + 16);
+    const uint64_t h4 = host_ns();
+    t_host[0] = h1 - h0; t_host[1] = h2 - h0; t_host[2] = h3 - h0; t_host[3] = h4 - h0;
     return st;
 }
 
@@ -702,6 +746,13 @@ extern "C" void noise_aead_debug_worker_stamps(uint32_t *out, int n)
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
     const WorkerSlot *s = g_worker[dev].slot;
     for (int i = 0; i < n && i < 5; ++i) out[i] = s ? s->stamps[i + 1] - s->stamps[0] : 0;
+}
+
+/* Test hook: this thread's last worker call on the host (ns from its
+   start): request packed, doorbell written, done seen, returned. */
+extern "C" void noise_aead_debug_worker_host_ns(uint64_t *out, int n)
+{
+    for (int i = 0; i < n && i < 4; ++i) out[i] = t_host[i];
 }
 
 /* Test hook: the latency-first path's s_memtime stamps (cycles from its

@@ -44,6 +44,7 @@ int main(int argc, char **argv)
     double ph[5] = {0, 0, 0, 0, 0}; /* resident-worker phase stamps (us), decrypt calls */
     double mhz = 0;                 /* the worker's shader clock while computing */
     double fs[6] = {0, 0, 0, 0, 0, 0}; /* latency-first path stamps (cycles), decrypt calls */
+    double hs[4] = {0, 0, 0, 0};       /* host side of the worker call (us), decrypt calls */
     int ok = 1;
     for (int it = -50; it < iters; ++it) { /* 50 untimed warm-up messages */
         NoiseBuffer b;
@@ -65,6 +66,9 @@ int main(int argc, char **argv)
             uint32_t f[6];
             noise_aead_debug_worker_fast_stamps(f, 6);
             for (int i = 0; i < 6; ++i) fs[i] += (double)f[i] / iters;
+            uint64_t hn[4];
+            noise_aead_debug_worker_host_ns(hn, 4);
+            for (int i = 0; i < 4; ++i) hs[i] += hn[i] * 1e-3 / iters;
         }
     }
     qsort(te, iters, sizeof(double), cmp_d);
@@ -75,10 +79,12 @@ int main(int argc, char **argv)
            "\"worker_phase_us\": {\"fence\": %.2f, \"inputs\": %.2f, \"computed\": %.2f, "
            "\"written\": %.2f, \"released\": %.2f}, \"worker_clock_mhz\": %.0f, "
            "\"fast_path_cycles\": {\"chacha\": %.0f, \"ct_in_lds\": %.0f, \"poly_loaded\": %.0f, "
-           "\"tree\": %.0f, \"tag\": %.0f, \"plaintext\": %.0f}, \"ok\": %s}\n",
+           "\"tree\": %.0f, \"tag\": %.0f, \"plaintext\": %.0f}, "
+           "\"host_us\": {\"packed\": %.2f, \"doorbell\": %.2f, \"done_seen\": %.2f, \"returned\": %.2f}, "
+           "\"ok\": %s}\n",
            name, len, iters, te[iters / 2], te[iters * 99 / 100], td[iters / 2],
            td[iters * 99 / 100], ph[0], ph[1], ph[2], ph[3], ph[4], mhz, fs[0], fs[1], fs[2], fs[3], fs[4], fs[5],
-           ok ? "true" : "false");
+           hs[0], hs[1], hs[2], hs[3], ok ? "true" : "false");
     noise_cipherstate_free(tx);
     noise_cipherstate_free(rx);
     return ok ? 0 : 1;
