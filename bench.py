@@ -328,7 +328,16 @@ def launch_ranks(n: int) -> int:
         port = so.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
-    return subprocess.run(cmd + sys.argv[1:]).returncode
+    # stdout carries exactly rank 0's JSON line; whatever else the ranks or
+    # their libraries print there (gloo's connection banner, ...) goes to stderr
+    proc = subprocess.Popen(cmd + sys.argv[1:], stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout:
+        if line.lstrip().startswith('{"metric"'):
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return proc.wait()
 
 
 def init_dist(world, local, dry_run):
