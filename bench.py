@@ -645,8 +645,11 @@ class UniformWork:
         # --streams 2 (separate mode): consecutive steps (independent batch
         # sets) alternate between two streams, so step s+1's seal can start on
         # CUs that step s's open is leaving.  Set b is reused every `sets` steps.
-        self.streams = [self.stream] + ([torch.cuda.Stream(dev)]
-                                        if args.streams == 2 and not self.duplex else [])
+        # With duplex steps the same alternation lets step s+1's launch fill
+        # the CUs step s's tail leaves (steps s and s+1 touch disjoint sets;
+        # steps s and s+2 share a stream, so the open of the set step s
+        # sealed stays ordered after it).
+        self.streams = [self.stream] + ([torch.cuda.Stream(dev)] if args.streams == 2 else [])
         self.opened = set()
 
     def _common(self):
@@ -668,7 +671,7 @@ class UniformWork:
                                   status=st.data_ptr(), flags=self.oflags,
                                   stream=stream or self.sp, **self._common())
 
-    def step_duplex(self, b, bo):
+    def step_duplex(self, b, bo, stream=None):
         A = self.A
         pt, ct, _, _ = self.sets[b]
         _, cto, back, st = self.sets[bo]
@@ -678,7 +681,7 @@ class UniformWork:
         oj = A.uniform_job(inp=cto.data_ptr(), out=back.data_ptr(), in_stride=self.out_stride,
                            out_stride=self.in_stride, status=st.data_ptr(), flags=self.oflags,
                            **self._common())
-        return A.dev_duplex(self.cipher, sj, oj, self.sp)
+        return A.dev_duplex(self.cipher, sj, oj, stream or self.sp)
 
     def untimed_step(self, w):
         """Step w outside the timed region (settle, warmup): the same launches."""
@@ -717,7 +720,7 @@ class UniformWork:
             b, bo = s % sets, (s - self.lag) % sets
             if self.duplex or not per_step:
                 if self.duplex:
-                    rc = self.step_duplex(b, bo)
+                    rc = self.step_duplex(b, bo, self.streams[s % len(self.streams)].cuda_stream)
                 else:
                     st_ = self.streams[s % len(self.streams)].cuda_stream
                     rc = self.seal(b, stream=st_) or self.open_(bo, stream=st_)
