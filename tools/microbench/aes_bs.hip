@@ -361,6 +361,132 @@ __global__ __launch_bounds__(256) BS_OCC void bs_ctr(const BsKey *__restrict__ K
     }
 }
 
+/* ------------------------------------------------ bitsliced, two lanes
+ * The same 32-block bitsliced state split over a lane pair: lane L holds
+ * state columns 2L and 2L+1 (64 VGPRs: local byte 4j + r, j = local column),
+ * so 128 VGPRs are enough for four waves per SIMD.  ShiftRows moves 4 of a
+ * lane's 8 bytes to its partner and back: with local column j the exchange
+ * is symmetric (both lanes want the partner's (1,0), (2,0), (2,1), (3,1)),
+ * one quad_perm [1,0,3,2] DPP per register.  Round-key masks depend on the
+ * lane's columns: read from LDS per lane. */
+NA_DEV uint32_t partner(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false); }
+
+/* one round on the lane's half state h[64]; mk: this lane's 64 masks */
+NA_DEV void bs2_round(uint32_t h[64], const uint32_t *mk, bool MIX)
+{
+#pragma unroll
+    for (int b = 0; b < 8; ++b) bs_sbox(h[8 * b], h[8 * b + 1], h[8 * b + 2], h[8 * b + 3], h[8 * b + 4],
+                                       h[8 * b + 5], h[8 * b + 6], h[8 * b + 7]);
+    /* the partner's (1,0), (2,0), (2,1), (3,1): local bytes 1, 2, 6, 7 */
+    uint32_t px[4][8];
+    const int pb[4] = {1, 2, 6, 7};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) px[i][k] = partner(h[8 * pb[i] + k]);
+    uint32_t o[64];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        /* a_r = byte (r, c + r) before ShiftRows, c = 2L + j */
+        const uint32_t *a[4];
+        a[0] = &h[8 * (4 * j + 0)];
+        a[1] = j == 0 ? &h[8 * (4 * 1 + 1)] : px[0];                 /* (1,1) own / (1,0) partner */
+        a[2] = j == 0 ? px[1] : px[2];                               /* (2,0) / (2,1) partner */
+        a[3] = j == 0 ? px[3] : &h[8 * (4 * 0 + 3)];                 /* (3,1) partner / (3,0) own */
+        uint32_t mkc[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) mkc[i] = mk[32 * j + i];
+        if (!MIX) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) o[8 * (4 * j + r) + k] = a[r][k] ^ mkc[8 * r + k];
+            continue;
+        }
+        uint32_t sx[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sx[k] = bs_x3(a[0][k], a[1][k], a[2][k]) ^ a[3][k];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t *A = a[r], *B = a[(r + 1) & 3];
+            uint32_t t[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] = A[k] ^ B[k];
+            uint32_t *O = &o[8 * (4 * j + r)];
+            const uint32_t *M = &mkc[8 * r];
+            O[0] = bs_x3(t[1], sx[0], A[0] ^ M[0]);
+            O[1] = bs_x3(t[2], sx[1], A[1] ^ M[1]);
+            O[2] = bs_x3(t[3], sx[2], A[2] ^ M[2]);
+            O[3] = bs_x3(t[4], t[0], bs_x3(sx[3], A[3], M[3]));
+            O[4] = bs_x3(t[5], t[0], bs_x3(sx[4], A[4], M[4]));
+            O[5] = bs_x3(t[6], sx[5], A[5] ^ M[5]);
+            O[6] = bs_x3(t[7], t[0], bs_x3(sx[6], A[6], M[6]));
+            O[7] = bs_x3(t[0], sx[7], A[7] ^ M[7]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) h[i] = o[i];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void bs2_ctr(
+    const BsKey *__restrict__ K, uint32_t n_hi, uint32_t n_lo, uint32_t ctr_base, uint32_t *out, uint64_t *clk)
+{
+    const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    /* masks by lane half: km[round][L][64] (columns 2L, 2L+1) */
+    __shared__ __align__(16) uint32_t km[15][2][64];
+    for (int i = threadIdx.x; i < 15 * 128; i += blockDim.x) {
+        const int rr = i / 128, b = (i % 128) / 8, k = i % 8; /* global byte b, bit k */
+        const int c = b / 4, r = b % 4, L = c / 2, j = c % 2;
+        km[rr][L][8 * (4 * j + r) + k] = K->m[rr][i % 128];
+    }
+    __syncthreads();
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t L = g & 1, pair = g >> 1;
+    const uint32_t ctr0 = ctr_base + 32u * pair;
+    /* this lane's bytes: global columns 2L, 2L+1 = state words 2L, 2L+1 */
+    const uint32_t wv[4] = {0u, n_hi, n_lo, ctr0};
+    uint32_t h[64];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t word = L ? wv[2 + j] : wv[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t byte = (word >> (24 - 8 * r)) & 255u;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[8 * (4 * j + r) + k] = 0u - ((byte >> (7 - k)) & 1u);
+        }
+    }
+    if (L) { /* byte 15 = (row 3, column 3): lane 1, local (3, j = 1) */
+        uint32_t *q = &h[8 * (4 * 1 + 3)];
+        q[7] = 0xAAAAAAAAu; q[6] = 0xCCCCCCCCu; q[5] = 0xF0F0F0F0u; q[4] = 0xFF00FF00u; q[3] = 0xFFFF0000u;
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) h[i] ^= km[0][L][i];
+#pragma unroll 1
+    for (int rr = 1; rr < 15; ++rr) bs2_round(h, km[rr][L], rr < 14);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        uint32_t r32[32];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r32[8 * rb + (7 - k)] = h[8 * (4 * j + rb) + k];
+        transpose32(r32);
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            if (MODE == 0) out[((size_t)pair * 32 + i) * 4 + 2 * L + j] = r32[i];
+            else acc ^= r32[i];
+        }
+    }
+    if (MODE == 1) out[g] = acc;
+    if (clk && threadIdx.x == 0) {
+        clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - c0;
+        clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
+    }
+}
+
 /* ------------------------------------------------------------ T-table */
 __global__ __launch_bounds__(GCM_WG) void tt_ctr(const uint32_t *__restrict__ rk_g, uint32_t n_hi, uint32_t n_lo,
                                                  uint32_t blocks_per_lane, uint32_t *out, int mode, uint64_t *clk)
@@ -457,6 +583,20 @@ int main(int argc, char **argv)
             if (memcmp(e, &h[blk * 4], 16)) { if (bad++ < 3) printf("bitsliced mismatch block %u: %08x vs %08x\n", blk, h[blk * 4], e[0]); }
         }
         printf("bitsliced check: %s (%d bad of %d)\n", bad ? "FAIL" : "ok", bad, 64 * 32);
+        hipLaunchKernelGGL((bs2_ctr<0>), dim3(1), dim3(64), 0, 0, dk, n_hi, n_lo, cb, dout, nullptr);
+        CK(hipMemcpy(h.data(), dout, 32 * 32 * 4 * 4, hipMemcpyDeviceToHost));
+        int bad3 = 0;
+        for (uint32_t blk = 0; blk < 32 * 32; ++blk) {
+            uint8_t s2[16] = {0, 0, 0, 0};
+            const uint32_t ctr = cb + blk;
+            for (int j = 0; j < 4; ++j) { s2[4 + j] = (uint8_t)(n_hi >> (24 - 8 * j)); s2[8 + j] = (uint8_t)(n_lo >> (24 - 8 * j)); s2[12 + j] = (uint8_t)(ctr >> (24 - 8 * j)); }
+            h_encrypt(rkb, s2);
+            uint32_t e[4];
+            memcpy(e, s2, 16);
+            if (memcmp(e, &h[blk * 4], 16)) { if (bad3++ < 3) printf("bitsliced-2 mismatch block %u: %08x vs %08x\n", blk, h[blk * 4], e[0]); }
+        }
+        printf("bitsliced two-lane check: %s (%d bad of %d)\n", bad3 ? "FAIL" : "ok", bad3, 32 * 32);
+        bad += bad3;
         const uint32_t bpl = 8;
         hipLaunchKernelGGL(tt_ctr, dim3(1), dim3(GCM_WG), sizeof(GcmLds), 0, drk, n_hi, n_lo, bpl, dout, 0, nullptr);
         std::vector<uint32_t> t(GCM_WG * bpl * 4);
@@ -479,7 +619,7 @@ int main(int argc, char **argv)
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
     uint64_t *dck;
-    CK(hipMalloc(&dck, 2 * 8192 * sizeof(uint64_t)));
+    CK(hipMalloc(&dck, 2 * 16384 * sizeof(uint64_t)));
     /* each kernel: ~0.4 s back to back first (the sustained-load clock,
        profiles/r03/clock_vs_warmup.log), then `reps` timed launches; the
        clock from s_memtime / s_memrealtime over every block of the last one */
@@ -504,6 +644,19 @@ int main(int argc, char **argv)
         const double bps = blocks1 * reps / (ms * 1e-3), mhz = clock_of(grid);
         printf("bitsliced: %.3f ms/launch, %.2f G blocks/s = %.1f GB/s keystream; %.2f SIMD-cycles/block at %.0f MHz (in-kernel)\n",
                ms / reps, bps * 1e-9, bps * 16e-9, 1024.0 * mhz * 1e6 / bps, mhz);
+    }
+    {
+        const int grid = 16384; /* 2 lanes per 32 blocks */
+        const double blocks1 = (double)grid * 256 / 2 * 32;
+        for (int w = 0; w < 400; ++w) hipLaunchKernelGGL((bs2_ctr<1>), dim3(grid), dim3(256), 0, 0, dk, n_hi, n_lo, 0u, dout, nullptr);
+        hipEventRecord(e0);
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((bs2_ctr<1>), dim3(grid), dim3(256), 0, 0, dk, n_hi, n_lo, 0u, dout, dck);
+        hipEventRecord(e1);
+        CK(hipEventSynchronize(e1));
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        const double bps = blocks1 * reps / (ms * 1e-3), mhz = clock_of(grid);
+        printf("bitsliced two-lane: %.3f ms/launch, %.2f G blocks/s; %.2f SIMD-cycles/block at %.0f MHz (in-kernel)\n",
+               ms / reps, bps * 1e-9, 1024.0 * mhz * 1e6 / bps, mhz);
     }
     {
         const int grid = 256 * 4; const uint32_t bpl = 256;
