@@ -80,15 +80,20 @@ NA_DEV void aes256_block(const uint32_t *__restrict__ rk, const uint32_t *te, co
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
 #pragma unroll
     for (int r = 1; r < 14; ++r) {
-        const uint32_t t0 = te[s0 >> 24] ^ rotr(te[(s1 >> 16) & 255], 8) ^
-                            rotr(te[(s2 >> 8) & 255], 16) ^ rotr(te[s3 & 255], 24) ^ rk[4 * r];
-        const uint32_t t1 = te[s1 >> 24] ^ rotr(te[(s2 >> 16) & 255], 8) ^
-                            rotr(te[(s3 >> 8) & 255], 16) ^ rotr(te[s0 & 255], 24) ^ rk[4 * r + 1];
-        const uint32_t t2 = te[s2 >> 24] ^ rotr(te[(s3 >> 16) & 255], 8) ^
-                            rotr(te[(s0 >> 8) & 255], 16) ^ rotr(te[s1 & 255], 24) ^ rk[4 * r + 2];
-        const uint32_t t3 = te[s3 >> 24] ^ rotr(te[(s0 >> 16) & 255], 8) ^
-                            rotr(te[(s1 >> 8) & 255], 16) ^ rotr(te[s2 & 255], 24) ^ rk[4 * r + 3];
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+        /* the round's 16 lookups are independent: issue them all, then one
+           wait (the empty asm keeps the scheduler from trading them for
+           registers one load at a time: 2x the block's latency in the
+           256-VGPR resident worker, tools/microbench/aes_lat.hip) */
+        uint32_t a0 = te[s0 >> 24], a1 = te[(s1 >> 16) & 255], a2 = te[(s2 >> 8) & 255], a3 = te[s3 & 255];
+        uint32_t b0 = te[s1 >> 24], b1 = te[(s2 >> 16) & 255], b2 = te[(s3 >> 8) & 255], b3 = te[s0 & 255];
+        uint32_t c0 = te[s2 >> 24], c1 = te[(s3 >> 16) & 255], c2 = te[(s0 >> 8) & 255], c3 = te[s1 & 255];
+        uint32_t d0 = te[s3 >> 24], d1 = te[(s0 >> 16) & 255], d2 = te[(s1 >> 8) & 255], d3 = te[s2 & 255];
+        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3),
+                          "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+        s0 = a0 ^ rotr(a1, 8) ^ rotr(a2, 16) ^ rotr(a3, 24) ^ rk[4 * r];
+        s1 = b0 ^ rotr(b1, 8) ^ rotr(b2, 16) ^ rotr(b3, 24) ^ rk[4 * r + 1];
+        s2 = c0 ^ rotr(c1, 8) ^ rotr(c2, 16) ^ rotr(c3, 24) ^ rk[4 * r + 2];
+        s3 = d0 ^ rotr(d1, 8) ^ rotr(d2, 16) ^ rotr(d3, 24) ^ rk[4 * r + 3];
     }
     const uint32_t o0 = (sb[s0 >> 24] << 24) | (sb[(s1 >> 16) & 255] << 16) |
                         (sb[(s2 >> 8) & 255] << 8) | sb[s3 & 255];
@@ -220,6 +225,35 @@ NA_DEV void gh_mul_lds(uint32_t y[4], const uint4 *tab)
         const uint4 f = tab[(p + 1) * 16 + (byte & 15)];
         r0 = xor3(r0, e.x, f.x); r1 = xor3(r1, e.y, f.y);
         r2 = xor3(r2, e.z, f.z); r3 = xor3(r3, e.w, f.w);
+    }
+    y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
+}
+
+/* gh_mul_lds for one wave's latency (the wide record's few GHASH lanes):
+   the lookups in two batches of 16, each issued whole before one wait */
+NA_DEV void gh_mul_lds_lat(uint32_t y[4], const uint4 *tab)
+{
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u *t4 = (const v4u *)tab;
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        v4u e[16];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int p = 16 * half + 2 * j, b = p >> 1;
+            const uint32_t byte = (y[b >> 2] >> (8 * (b & 3))) & 255u;
+            e[2 * j] = t4[p * 16 + (byte >> 4)];
+            e[2 * j + 1] = t4[(p + 1) * 16 + (byte & 15)];
+        }
+        asm volatile("" : "+v"(e[0]), "+v"(e[1]), "+v"(e[2]), "+v"(e[3]), "+v"(e[4]), "+v"(e[5]), "+v"(e[6]),
+                          "+v"(e[7]), "+v"(e[8]), "+v"(e[9]), "+v"(e[10]), "+v"(e[11]), "+v"(e[12]), "+v"(e[13]),
+                          "+v"(e[14]), "+v"(e[15]));
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) {
+            r0 = xor3(r0, e[j].x, e[j + 1].x); r1 = xor3(r1, e[j].y, e[j + 1].y);
+            r2 = xor3(r2, e[j].z, e[j + 1].z); r3 = xor3(r3, e[j].w, e[j + 1].w);
+        }
     }
     y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
 }
@@ -1127,50 +1161,78 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
 /* ------------------------------------------ wide (small batches, latency)
  *
  * One record per 256-thread workgroup, for batches of at most 512 records
- * (the single-call path of noise_cipherstate_*, short wire buffers).  The record's CTR blocks are spread over all 256
- * threads; GHASH is gcm_record's 4-lane Horner (H^4 steps, scale by
- * H^(4-l), XOR-reduce) run by lanes 0..3 with the H^4 table in LDS.  Seal:
- * CTR, then GHASH over the CT just written.  Open: GHASH and tag check
- * first, CTR only when the tag verified (cipher-aesgcm.c:184-186).
+ * (the single-call path of noise_cipherstate_*, short wire buffers), and the
+ * resident worker's AES-GCM records.  Latency first: counter block v + 1 is
+ * "virtual block" v, v = 0 being E_K(J0) (the tag mask, cipher-aesgcm.c:
+ * 99-125) and v >= 1 data block v - 1, so E_K(J0) comes out of the same
+ * SIMT pass as the CTR blocks instead of after GHASH.  GHASH is gcm_record's
+ * K-lane Horner (H^K steps, scale by H^(K-l), XOR-reduce; K = 8 with the
+ * H^8 table) run by lanes 0..K-1 of wave 0, the table in LDS.
+ *   Seal: CTR (and E_K(J0)), then GHASH over the CT just written.
+ *   Open: waves 1-3 compute E_K(J0) and the first 191 keystream blocks
+ *   while wave 0 runs GHASH; the tag is checked first and the keystream
+ *   applied only when it verified (cipher-aesgcm.c:184-186): no plaintext
+ *   byte of a rejected record is ever written.
  */
 /* One record on a 256-thread workgroup (the whole workgroup calls it):
-   te/sb/h4 are the LDS tables (h4: the record's H^4 multiply table when not
-   CT), verdict an LDS word.  Returns (open) whether the tag verified; writes
-   status when given; a rejected record's output is left alone here (the
-   caller scrubs).  Shared by gcm_wide and the resident worker (worker.hip). */
-template <bool OPEN, bool CT>
+   te/sb/hk are the LDS tables (hk: the record's H^K multiply table when not
+   CT), wl five LDS words (verdict, E_K(J0)).  Returns (open) whether the tag
+   verified; writes status when given; a rejected record's output is left
+   alone here (the caller scrubs).  Shared by gcm_wide and the resident
+   worker (worker.hip); dbg, when given, takes thread 0's s_memtime stamps. */
+template <bool OPEN, bool CT, int K = 8>
 NA_DEV bool gcm_wide_record(const uint8_t *src, uint8_t *dst, const uint8_t *ad, uint32_t ad_len,
                             uint32_t len, uint64_t nonce, const AesCtx *ctx, const uint32_t *te,
-                            const uint32_t *sb, const uint4 *h4, uint32_t *verdict, uint8_t *status)
+                            const uint32_t *sb, const uint4 *hk, uint32_t *wl, uint8_t *status,
+                            uint32_t *dbg = nullptr)
 {
-    constexpr int K = GCM_LANES;
+    static_assert(K == 4 || K == 8, "GHASH lanes: 4 (H^4) or 8 (H^8)");
+#define NA_GSTAMP(k) do { if (dbg && threadIdx.x == 0) dbg[k] = (uint32_t)__builtin_amdgcn_s_memtime(); } while (0)
+    constexpr uint32_t EARLY = 192; /* open: virtual blocks 0..191 run beside GHASH (waves 1-3) */
     const uint32_t t = threadIdx.x, M = (len + 15) / 16;
     const uint32_t *rk = ctx->rk;
+    uint32_t ks[4] = {0, 0, 0, 0};
+    bool early = false;
     if (!OPEN) {
-        for (uint32_t b = t; b < M; b += 256) {
-            const uint32_t nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
-            uint32_t x[4], ks[4];
-            load16(src + 16 * b, nb, x);
-            aes_ctr_block(rk, te, sb, nonce, 2 + b, ks);
+        for (uint32_t v = t; v <= M; v += 256) {
+            aes_ctr_block(rk, te, sb, nonce, v + 1, ks);
+            if (v == 0) {
+                wl[1] = ks[0]; wl[2] = ks[1]; wl[3] = ks[2]; wl[4] = ks[3];
+            } else {
+                const uint32_t b = v - 1, nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
+                uint32_t x[4];
+                load16(src + 16 * b, nb, x);
 #pragma unroll
-            for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
-            store16(dst + 16 * b, nb, x);
+                for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+                store16(dst + 16 * b, nb, x);
+            }
         }
-        __syncthreads(); /* the GHASH lanes read this CT back (same CU) */
+    } else if (t >= 64) {
+        const uint32_t v = t - 64;
+        early = v <= M && v < EARLY;
+        if (dbg && t == 64) dbg[6] = (uint32_t)__builtin_amdgcn_s_memtime();
+        if (early) aes_ctr_block(rk, te, sb, nonce, v + 1, ks);
+        if (dbg && t == 64) dbg[7] = (uint32_t)__builtin_amdgcn_s_memtime();
+        if (v == 0) { wl[1] = ks[0]; wl[2] = ks[1]; wl[3] = ks[2]; wl[4] = ks[3]; }
     }
+    if (!OPEN) __syncthreads(); /* the GHASH lanes read this CT back (same CU) */
+    NA_GSTAMP(0);
+    uint32_t acc[4] = {0, 0, 0, 0};
     if (t < (uint32_t)K) {
         const int l = (int)t;
         const uint8_t *ct = OPEN ? src : dst;
         const uint32_t A = (ad_len + 15) / 16, n = A + M + 1;
         const uint32_t c0 = ((uint32_t)l + n) % K;
-        uint32_t h4n[4] = {0, 0, 0, 0};
+        uint32_t hkn[4] = {0, 0, 0, 0};
         if constexpr (CT) {
 #pragma unroll
-            for (int w = 0; w < 4; ++w) h4n[w] = ctx->hn[K - 1][w];
+            for (int w = 0; w < 4; ++w) hkn[w] = K == 8 ? ctx->hn8[w] : ctx->hn[K - 1][w];
         }
-        uint32_t acc[4] = {0, 0, 0, 0};
         for (uint32_t i = c0; i < n; i += K) {
-            if (i != c0) gh_step<CT>(acc, h4, h4n);
+            if (i != c0) {
+                if constexpr (CT) gh_mul_ct(acc, hkn);
+                else gh_mul_lds_lat(acc, hk);
+            }
             uint32_t x[4];
             if (i < A) {
                 const uint32_t rem = ad_len - 16 * i;
@@ -1186,49 +1248,64 @@ NA_DEV bool gcm_wide_record(const uint8_t *src, uint8_t *dst, const uint8_t *ad,
             if constexpr (CT) gh_to_nat(x);
             acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
         }
-        gh_scale<CT>(acc, ctx, K - 1 - l);
+        NA_GSTAMP(1);
+        gh_scale<CT, K>(acc, ctx, K - 1 - l);
 #pragma unroll
         for (int off = 1; off < K; off <<= 1)
 #pragma unroll
             for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
         if constexpr (CT) gh_to_nat(acc);
-        uint32_t ej[4];
-        aes_ctr_block(rk, te, sb, nonce, 1u, ej);
-        const uint32_t tag[4] = {acc[0] ^ ej[0], acc[1] ^ ej[1], acc[2] ^ ej[2], acc[3] ^ ej[3]};
-        if (!OPEN) {
-            if (l == K - 1) store16(dst + len, 16, tag);
-            if (l == K - 1 && status) *status = 0;
-        } else if (l == 0) {
-            uint32_t got[4];
-            load16(src + len, 16, got);
-            const bool ok = ((tag[0] ^ got[0]) | (tag[1] ^ got[1]) | (tag[2] ^ got[2]) |
-                             (tag[3] ^ got[3])) == 0;
-            *verdict = ok;
-            if (status) *status = ok ? 0 : 1;
-        }
+        NA_GSTAMP(2);
     }
-    if (!OPEN) return true;
+    if (OPEN) __syncthreads(); /* E_K(J0) from wave 1 */
+    NA_GSTAMP(3);
+    if (!OPEN) {
+        if (t == (uint32_t)K - 1) {
+            const uint32_t tag[4] = {acc[0] ^ wl[1], acc[1] ^ wl[2], acc[2] ^ wl[3], acc[3] ^ wl[4]};
+            store16(dst + len, 16, tag);
+            if (status) *status = 0;
+        }
+        return true;
+    }
+    if (t == 0) {
+        uint32_t got[4];
+        load16(src + len, 16, got);
+        const bool ok = ((acc[0] ^ wl[1] ^ got[0]) | (acc[1] ^ wl[2] ^ got[1]) | (acc[2] ^ wl[3] ^ got[2]) |
+                         (acc[3] ^ wl[4] ^ got[3])) == 0;
+        wl[0] = ok;
+        if (status) *status = ok ? 0 : 1;
+    }
     __syncthreads();
-    if (!*verdict) return false; /* nothing decrypted */
-    for (uint32_t b = t; b < M; b += 256) {
+    NA_GSTAMP(4);
+    if (!wl[0]) return false; /* nothing decrypted */
+    if (early && t > 64) { /* keystream block t - 65, computed beside GHASH */
+        const uint32_t b = t - 65, nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
+        uint32_t x[4];
+        load16(src + 16 * b, nb, x);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
+        store16(dst + 16 * b, nb, x);
+    }
+    for (uint32_t b = EARLY - 1 + t; b < M; b += 256) {
         const uint32_t nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
-        uint32_t x[4], ks[4];
+        uint32_t x[4];
         load16(src + 16 * b, nb, x);
         aes_ctr_block(rk, te, sb, nonce, 2 + b, ks);
 #pragma unroll
         for (int w = 0; w < 4; ++w) x[w] ^= ks[w];
         store16(dst + 16 * b, nb, x);
     }
+    NA_GSTAMP(5);
+#undef NA_GSTAMP
     return true;
 }
 
 template <bool OPEN, bool CT>
 __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
 {
-    constexpr int K = GCM_LANES;
     __shared__ uint32_t te[256], sb[256];
-    __shared__ uint4 h4[GHASH_TAB_ENTRIES];
-    __shared__ uint32_t verdict;
+    __shared__ uint4 h8[GHASH_TAB_ENTRIES];
+    __shared__ uint32_t wl[5];
     const uint32_t rec = blockIdx.x, t = threadIdx.x;
     const RecDesc d = a.recs[rec];
     if (reject_len(a, rec, d.len, t == 0)) return; /* uniform over the workgroup */
@@ -1241,10 +1318,10 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
     }
     if (!CT)
         for (uint32_t i = t; i < (uint32_t)GHASH_TAB_ENTRIES; i += 256)
-            h4[i] = ((const uint4 *)ctx->tab[K - 1])[i];
+            h8[i] = ((const uint4 *)ctx->tab8)[i];
     __syncthreads();
     const bool ok = gcm_wide_record<OPEN, CT>(src, dst, a.ad + d.ad_off, d.ad_len, d.len, d.nonce, ctx,
-                                              te, sb, h4, &verdict, a.status ? a.status + rec : nullptr);
+                                              te, sb, h8, wl, a.status ? a.status + rec : nullptr);
     if (OPEN && !ok && !a.vf) scrub_rejected(dst, src, d.len, t, 256);
 }
 

@@ -6,8 +6,11 @@
  * Launching a kernel and waiting for it costs ~20 us on its own, 5x the
  * reference's whole ~4 us CPU call.  Instead, the first call on a device
  * starts ONE resident workgroup (256 threads) on a private stream; it polls
- * a request slot in pinned, fine-grained host memory and serves records as
- * they are posted:
+ * a request slot and serves records as they are posted.  The request (header
+ * and input stream) sits in fine-grained device memory that the CPU writes
+ * through the BAR where the device has a large BAR, else in pinned host
+ * memory; results, status and the done word always go to pinned host memory,
+ * so each side polls memory of its own and writes the other's:
  *
  *   host                                    worker (aead_worker)
  *   write AD || record || tag to data[]
@@ -70,9 +73,16 @@ constexpr uint32_t WORKER_HEAD = WORKER_SPEC * WCHUNK_BYTES; /* stream bytes sen
 /* the stream past the head (records over ~3 KiB) is posted raw, read after the header */
 constexpr uint32_t WORKER_TAIL = WORKER_DATA - WORKER_HEAD;
 static_assert(WORKER_HEAD % 16 == 0, "the raw tail lands 16-B aligned in LDS");
+/* With the request in device memory the CPU's stores reach it through
+   write-combining buffers, which may write a 16-byte store as two 8-byte
+   pieces: there every 8-byte half carries the number, {4 stream bytes, seq}
+   (header chunks {seq, field, seq, field}), so a chunk is 8 stream bytes. */
+constexpr uint32_t VCHUNK_BYTES = 8;
+constexpr uint32_t VWORKER_HEAD = WORKER_SPEC * VCHUNK_BYTES;
+constexpr uint32_t VWORKER_TAIL = WORKER_DATA - VWORKER_HEAD;
 /* AES-GCM contexts the worker keeps in LDS (an echo session uses two) */
 constexpr int WORKER_CTX_SLOTS = 2;
-constexpr uint32_t WORKER_CTX_BYTES = offsetof(AesCtx, tab8); /* rk, H, H^1..H^4 */
+constexpr uint32_t WORKER_CTX_BYTES = sizeof(AesCtx); /* rk, H, the H^1..H^4 and H^8 tables */
 
 /* The request slot (host pinned, fine-grained).  The request header is four
    16-byte chunks, each starting with the request's sequence number; the host
@@ -349,18 +359,31 @@ NA_DEV void load_sys16x2(const uint32_t *p, const uint32_t *q, uint4 &a, uint4 &
 
 NA_DEV uint32_t now10ns() { return (uint32_t)__builtin_amdgcn_s_memrealtime(); }
 
-/* 256 threads.  last: the last request already served; idle/lifetime in
-   s_memrealtime ticks (100 MHz). */
-__global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint4 *in, const uint8_t *tail,
-                                                   uint8_t *out, uint32_t last, uint64_t idle,
-                                                   uint64_t lifetime)
+/* 16 raw stream bytes, system-coherent, as two 8-byte atomic loads the
+   compiler schedules (no wait per load) */
+NA_DEV uint4 load_sys16_raw(const uint8_t *p)
 {
+    const uint64_t *q = (const uint64_t *)p;
+    const uint64_t a = NA_SYS_LOAD(q), b = NA_SYS_LOAD(q + 1);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+
+/* 256 threads.  req: the header chunks (4 in host memory; 8 in device
+   memory, vram); in: the stream's stamped chunks, tail: the rest raw; last:
+   the last request already served; idle/lifetime in s_memrealtime ticks
+   (100 MHz). */
+__global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint32_t *req, const uint4 *in,
+                                                   uint32_t vram, const uint8_t *tail, uint8_t *out,
+                                                   uint32_t last, uint64_t idle, uint64_t lifetime)
+{
+    const uint32_t head = vram ? VWORKER_HEAD : WORKER_HEAD, cbytes = vram ? VCHUNK_BYTES : WCHUNK_BYTES;
     __shared__ uint32_t te[256], sb[256];
     __shared__ __attribute__((aligned(16))) uint8_t cbuf[WORKER_CTX_SLOTS][WORKER_CTX_BYTES];
     __shared__ uint64_t ctag[WORKER_CTX_SLOTS]; /* host address of the cached context */
     __shared__ uint32_t cgen[WORKER_CTX_SLOTS], cuse[WORKER_CTX_SLOTS];
     __shared__ uint32_t hdr[16];
     __shared__ uint32_t verdict, s_cmd; /* s_cmd: 0 wait, 1 serve, 2 leave */
+    __shared__ uint32_t wl[5];          /* gcm_wide_record's verdict and E_K(J0) */
     __shared__ uint32_t s_stale;        /* chunks still stamped with an older request */
     __shared__ FastLds fast;
     __shared__ __attribute__((aligned(16))) uint8_t buf[WORKER_DATA];
@@ -377,18 +400,35 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint4
     uint32_t tick = 0;
     for (;;) {
         uint32_t t_seen = 0;
-        /* every thread reads input chunk t; wave 0's lanes 0..3 hold the
-           header (other lanes read a header chunk too: same round trip) */
+        /* every thread reads input chunk t; wave 0's lanes 0..3 (0..7 in
+           device memory) hold the header (other lanes read a header chunk
+           too: same round trip) */
         uint4 c, mine;
-        load_sys16x2(slot->c0 + 4 * (t & 3), (const uint32_t *)(in + t), c, mine);
+        load_sys16x2(req + 4 * (t & (vram ? 7 : 3)), (const uint32_t *)(in + t), c, mine);
         if (t == 0) s_stale = 0;
         if (t < 64) {
-            const uint32_t s0 = __shfl((int)c.x, 0, 64), s1 = __shfl((int)c.x, 1, 64);
-            const uint32_t s2 = __shfl((int)c.x, 2, 64), s3 = __shfl((int)c.x, 3, 64);
-            const uint32_t stop = __shfl((int)c.w, 2, 64);
-            const bool fresh = s0 != last && s0 == s1 && s0 == s2 && s0 == s3;
-            if (t < 4) {
-                hdr[4 * t] = c.x; hdr[4 * t + 1] = c.y; hdr[4 * t + 2] = c.z; hdr[4 * t + 3] = c.w;
+            const uint32_t s0 = __shfl((int)c.x, 0, 64);
+            uint32_t stop;
+            bool fresh;
+            if (!vram) { /* chunk k = {seq, A_k, B_k, C_k} */
+                const uint32_t s1 = __shfl((int)c.x, 1, 64);
+                const uint32_t s2 = __shfl((int)c.x, 2, 64), s3 = __shfl((int)c.x, 3, 64);
+                stop = __shfl((int)c.w, 2, 64);
+                fresh = s0 != last && s0 == s1 && s0 == s2 && s0 == s3;
+                if (t < 4) {
+                    hdr[4 * t] = c.x; hdr[4 * t + 1] = c.y; hdr[4 * t + 2] = c.z; hdr[4 * t + 3] = c.w;
+                }
+            } else { /* chunk 2k = {seq, A_k, seq, B_k}, 2k + 1 = {seq, C_k, seq, 0} */
+                stop = __shfl((int)c.y, 5, 64);
+                fresh = s0 != last && __all(t >= 8 || (c.x == s0 && c.z == s0));
+                if (t < 8) {
+                    const uint32_t k = t >> 1;
+                    if (t & 1) {
+                        hdr[4 * k + 3] = c.y;
+                    } else {
+                        hdr[4 * k] = c.x; hdr[4 * k + 1] = c.y; hdr[4 * k + 2] = c.w;
+                    }
+                }
             }
             if (t == 0) {
                 uint32_t cmd = 0;
@@ -433,17 +473,21 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint4
            speculatively with the poll, re-read while stale), the rest raw
            (written before the header, read after it) */
         const uint32_t total = 32 + ad_pad + len + (op ? 16u : 0u);
-        const uint32_t nchunks = min((total + WCHUNK_BYTES - 1) / WCHUNK_BYTES, WORKER_SPEC);
+        const uint32_t nchunks = min((total + cbytes - 1) / cbytes, WORKER_SPEC);
         if (t < nchunks) {
             uint4 v = mine;
-            for (uint32_t tries = 0; v.w != seq && tries < (1u << 20); ++tries)
+            for (uint32_t tries = 0; (v.w != seq || (vram && v.y != seq)) && tries < (1u << 20); ++tries)
                 v = load_sys16((const uint32_t *)(in + t));
-            if (v.w != seq) s_stale = 1; /* never in practice: the host wrote it before the header */
-            uint32_t *d = (uint32_t *)(buf + WCHUNK_BYTES * t);
-            d[0] = v.x; d[1] = v.y; d[2] = v.z;
+            if (v.w != seq || (vram && v.y != seq)) s_stale = 1; /* never in practice: written before the header */
+            uint32_t *d = (uint32_t *)(buf + cbytes * t);
+            if (vram) {
+                d[0] = v.x; d[1] = v.z;
+            } else {
+                d[0] = v.x; d[1] = v.y; d[2] = v.z;
+            }
         }
-        for (uint32_t o = 16 * t; WORKER_HEAD + o < total; o += 16 * 256)
-            *(uint4 *)(buf + WORKER_HEAD + o) = *(const uint4 *)(tail + o);
+        for (uint32_t o = 16 * t; head + o < total; o += 16 * 256)
+            *(uint4 *)(buf + head + o) = load_sys16_raw(tail + o);
         int cs = 0;
         if (cipher == NOISE_CIPHER_AESGCM) { /* the context: cached, or copied into the LRU slot */
             cs = ctag[0] == ctx_addr && cgen[0] == gen ? 0 : (ctag[1] == ctx_addr && cgen[1] == gen ? 1 : -1);
@@ -461,6 +505,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint4
             cuse[cs] = ++tick;
         }
         const uint32_t t_in = now10ns();
+        if (t < 8) fast.dbg[t] = 0; /* the path's stamps: those it does not reach stay 0 */
         const uint64_t c_in = __builtin_amdgcn_s_memtime();
         uint8_t *key = buf, *ad = buf + 32, *rec = buf + 32 + ad_pad;
         bool ok = true;
@@ -490,12 +535,14 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint4
             __syncthreads();
             ok = verdict != 0;
         } else {
-            const AesCtx *c = (const AesCtx *)cbuf[cs]; /* fields before tab8 only */
-            const uint4 *h4 = (const uint4 *)c->tab[GCM_LANES - 1];
-            if (ct) ok = op ? gcm_wide_record<true, true>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h4, &verdict, nullptr)
-                            : gcm_wide_record<false, true>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h4, &verdict, nullptr);
-            else ok = op ? gcm_wide_record<true, false>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h4, &verdict, nullptr)
-                         : gcm_wide_record<false, false>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h4, &verdict, nullptr);
+            const AesCtx *c = (const AesCtx *)cbuf[cs];
+            const uint4 *h8 = (const uint4 *)c->tab8;
+            if (ct) ok = op ? gcm_wide_record<true, true>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h8, wl, nullptr, fast.dbg)
+                            : gcm_wide_record<false, true>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h8, wl, nullptr, fast.dbg);
+            else ok = op ? gcm_wide_record<true, false>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h8, wl, nullptr, fast.dbg)
+                         : gcm_wide_record<false, false>(rec, rec, ad, ad_len, len, nonce, c, te, sb, h8, wl, nullptr, fast.dbg);
+            if (t == 0) /* absolute s_memtime stamps -> cycles since c_in */
+                for (int k = 0; k < 8; ++k) fast.dbg[k] = fast.dbg[k] ? fast.dbg[k] - (uint32_t)c_in : 0u;
         }
         __syncthreads();
         const uint32_t t_done = now10ns();
@@ -546,6 +593,12 @@ struct Worker {
     int state = 0;             /* 0 unknown, 1 usable, -1 disabled */
     WorkerSlot *slot = nullptr; /* host view */
     WorkerSlot *dslot = nullptr; /* device view */
+    /* the request (header chunks, stream): in fine-grained device memory the
+       CPU writes through the BAR (vram), or in the host slot */
+    bool vram = false;
+    uint32_t *req = nullptr;    /* host view of the header chunks */
+    const uint32_t *dreq = nullptr;
+    void *vbase = nullptr;      /* the device allocation (vram) */
     uint4 *in = nullptr, *din = nullptr;       /* the stream's head: stamped chunks */
     uint8_t *tail = nullptr, *dtail = nullptr; /* the rest of the stream, raw */
     uint8_t *out = nullptr, *dout = nullptr;   /* raw results */
@@ -561,13 +614,17 @@ std::once_flag g_atexit_once;
 constexpr uint64_t IDLE_TICKS = 200000;       /* 2 ms at 100 MHz */
 constexpr uint64_t LIFETIME_TICKS = 500000000; /* 5 s */
 
+/* the header's stop field: chunk 2 word 3 (host memory), chunk 5 word 1 (device) */
+uint32_t *stop_word(Worker &w) { return w.vram ? &w.req[4 * 5 + 1] : &w.req[4 * 2 + 3]; }
+
 void worker_stop_all()
 {
     for (int d = 0; d < kMaxDev; ++d) {
         Worker &w = g_worker[d];
         std::lock_guard<std::mutex> lk(w.mu);
         if (w.state != 1 || !w.launched) continue;
-        __atomic_store_n(&w.slot->c2[3], 1u, __ATOMIC_RELEASE); /* stop */
+        __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
+        _mm_sfence();
         (void)hipStreamSynchronize(w.stream);
         w.launched = false;
     }
@@ -582,7 +639,21 @@ bool worker_enabled()
     return v != 0;
 }
 
-int worker_setup(Worker &w)
+/* The request goes to device memory when the CPU can store to it (a large
+   BAR: hipDeviceAttributeIsLargeBar): the worker then polls its own HBM and
+   the host's stores arrive as posted PCIe writes, ordered behind each other
+   (tools/microbench/doorbell.hip: 1 KiB request + doorbell -> acknowledgement
+   3.2 us vs 4.9-5.5 us polling host memory).  NOISE_AEAD_WORKER_VRAM=0 keeps
+   it in host memory. */
+bool vram_wanted(int dev)
+{
+    const char *e = getenv("NOISE_AEAD_WORKER_VRAM");
+    if (e && e[0] == '0') return false;
+    int large_bar = 0;
+    return hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) == hipSuccess && large_bar;
+}
+
+int worker_setup(Worker &w, int dev)
 {
     if (w.state) return w.state;
     w.state = -1;
@@ -598,6 +669,19 @@ int worker_setup(Worker &w)
     w.dtail = (uint8_t *)(w.din + WORKER_SPEC);
     w.out = w.tail + tail_bytes;
     w.dout = w.dtail + tail_bytes;
+    w.req = w.slot->c0;
+    w.dreq = w.dslot->c0;
+    /* device-memory request: 8 header chunks (128 B), the stamped chunks, then the raw tail */
+    const size_t vbytes = 128 + in_bytes + VWORKER_TAIL + 64;
+    if (vram_wanted(dev) && hipExtMallocWithFlags(&w.vbase, vbytes, hipDeviceMallocFinegrained) == hipSuccess) {
+        memset(w.vbase, 0, vbytes); /* through the BAR mapping */
+        _mm_sfence();
+        w.vram = true;
+        w.req = (uint32_t *)w.vbase;
+        w.dreq = (const uint32_t *)w.vbase;
+        w.in = w.din = (uint4 *)((uint8_t *)w.vbase + 128);
+        w.tail = w.dtail = (uint8_t *)(w.in + WORKER_SPEC);
+    }
     if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess) return -1;
     std::call_once(g_atexit_once, [] { atexit(worker_stop_all); });
     w.state = 1;
@@ -608,9 +692,10 @@ int worker_launch(Worker &w)
 {
     (void)hipStreamSynchronize(w.stream); /* a previous worker has left */
     __atomic_store_n(&w.slot->exiting, 0u, __ATOMIC_RELEASE);
-    __atomic_store_n(&w.slot->c2[3], 0u, __ATOMIC_RELEASE); /* stop */
-    hipLaunchKernelGGL(aead_worker, dim3(1), dim3(256), 0, w.stream, w.dslot, (const uint4 *)w.din,
-                       (const uint8_t *)w.dtail, w.dout, w.seq, IDLE_TICKS, LIFETIME_TICKS);
+    __atomic_store_n(stop_word(w), 0u, __ATOMIC_RELEASE);
+    _mm_sfence();
+    hipLaunchKernelGGL(aead_worker, dim3(1), dim3(256), 0, w.stream, w.dslot, w.dreq, (const uint4 *)w.din,
+                       w.vram ? 1u : 0u, (const uint8_t *)w.dtail, w.dout, w.seq, IDLE_TICKS, LIFETIME_TICKS);
     if (hipGetLastError() != hipSuccess) return NOISE_ERROR_SYSTEM;
     w.launched = true;
     return NOISE_ERROR_NONE;
@@ -670,7 +755,7 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return NOISE_ERROR_NOT_APPLICABLE;
     Worker &w = g_worker[dev];
     std::lock_guard<std::mutex> lk(w.mu);
-    if (worker_setup(w) != 1) return NOISE_ERROR_NOT_APPLICABLE;
+    if (worker_setup(w, dev) != 1) return NOISE_ERROR_NOT_APPLICABLE;
     void *d_hctx = nullptr;
     if (h_ctx && hipHostGetDevicePointer(&d_hctx, (void *)h_ctx, 0) != hipSuccess)
         return NOISE_ERROR_NOT_APPLICABLE;
@@ -681,31 +766,55 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
         if (rc) return rc;
     }
     const uint32_t k = ++w.seq;
-    /* the input stream key || AD || pad || record (|| tag): its first
-       WORKER_HEAD bytes as stamped chunks (12 stream bytes + k), the rest raw */
+    /* the input stream key || AD || pad || record (|| tag): its first head
+       bytes as stamped chunks, the rest raw.  Host memory: 12 stream bytes +
+       k per chunk; device memory: {4 bytes, k, 4 bytes, k} */
     const size_t in_len = len + (open ? 16 : 0), total = 32 + ad_pad + in_len;
-    const size_t head = total < WORKER_HEAD ? total : WORKER_HEAD;
-    const size_t nchunks = (head + WCHUNK_BYTES - 1) / WCHUNK_BYTES;
+    const size_t cbytes = w.vram ? VCHUNK_BYTES : WCHUNK_BYTES;
+    const size_t hmax = w.vram ? VWORKER_HEAD : WORKER_HEAD;
+    const size_t head = total < hmax ? total : hmax;
+    const size_t nchunks = (head + cbytes - 1) / cbytes;
+    const __m128i keep = _mm_set_epi32(0, -1, -1, -1), stamp = _mm_set_epi32((int)k, 0, 0, 0);
+    const __m128i kk = _mm_set1_epi32((int)k);
+    const __m128i vstamp = _mm_set_epi32((int)k, 0, (int)k, 0); /* a scrubbed device chunk */
     alignas(16) uint8_t tmp[WORKER_HEAD + 16];
     memset(tmp, 0, 32 + ad_pad);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) memcpy(tmp, key, 32);
     if (ad_len) memcpy(tmp + 32, ad, ad_len);
     memcpy(tmp + 32 + ad_pad, data, head - 32 - ad_pad);
     memset(tmp + head, 0, 16); /* the last chunk's bytes past the stream */
-    const __m128i keep = _mm_set_epi32(0, -1, -1, -1), stamp = _mm_set_epi32((int)k, 0, 0, 0);
-    for (size_t c = 0; c < nchunks; ++c) {
-        const __m128i v = _mm_loadu_si128((const __m128i *)(tmp + WCHUNK_BYTES * c));
-        _mm_store_si128((__m128i *)(w.in + c), _mm_or_si128(_mm_and_si128(v, keep), stamp));
+    if (w.vram) {
+        for (size_t c = 0; c < nchunks; ++c) {
+            const __m128i v = _mm_loadl_epi64((const __m128i *)(tmp + VCHUNK_BYTES * c));
+            _mm_store_si128((__m128i *)(w.in + c), _mm_unpacklo_epi32(v, kk)); /* {b0, k, b1, k} */
+        }
+    } else {
+        for (size_t c = 0; c < nchunks; ++c) {
+            const __m128i v = _mm_loadu_si128((const __m128i *)(tmp + WCHUNK_BYTES * c));
+            _mm_store_si128((__m128i *)(w.in + c), _mm_or_si128(_mm_and_si128(v, keep), stamp));
+        }
     }
     explicit_bzero(tmp, head);
     if (total > head) memcpy(w.tail, data + (head - 32 - ad_pad), total - head);
     const uint64_t ctx = (uint64_t)(uintptr_t)d_hctx;
     const uint64_t h1 = host_ns();
-    __atomic_thread_fence(__ATOMIC_RELEASE); /* the data area before the header */
-    store_chunk(s->c0, k, (open ? 1u : 0u) | (ct_env() ? 1u << 8 : 0u), (uint32_t)len, (uint32_t)ad_len);
-    store_chunk(s->c1, k, (uint32_t)nonce, (uint32_t)(nonce >> 32), (uint32_t)cipher_id);
-    store_chunk(s->c2, k, (uint32_t)ctx, (uint32_t)(ctx >> 32), 0u);
-    store_chunk(s->c3, k, gen, 0u, 0u);
+    /* the data area before the header: sfence drains the write-combining
+       buffers (device memory) and orders the stores (both) */
+    _mm_sfence();
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    const uint32_t f[4][3] = {{(open ? 1u : 0u) | (ct_env() ? 1u << 8 : 0u), (uint32_t)len, (uint32_t)ad_len},
+                              {(uint32_t)nonce, (uint32_t)(nonce >> 32), (uint32_t)cipher_id},
+                              {(uint32_t)ctx, (uint32_t)(ctx >> 32), 0u},
+                              {gen, 0u, 0u}};
+    for (int c = 0; c < 4; ++c) {
+        if (w.vram) { /* chunk 2c = {k, A, k, B}, 2c + 1 = {k, C, k, 0} */
+            store_chunk(w.req + 8 * c, k, f[c][0], k, f[c][1]);
+            store_chunk(w.req + 8 * c + 4, k, f[c][2], k, 0u);
+        } else {
+            store_chunk(w.req + 4 * c, k, f[c][0], f[c][1], f[c][2]);
+        }
+    }
+    _mm_sfence(); /* out of the write-combining buffer now, not later */
     const uint64_t h2 = host_ns();
     uint64_t spins = 0;
     while (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
@@ -728,8 +837,9 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     if (st == NOISE_ERROR_NONE) memcpy(data, w.out, open ? len : len + 16);
     /* key, plaintext and results out of the shared host memory; the stamps
        stay (a zeroed chunk would carry number 0, which no request has) */
-    for (size_t c = 0; c < nchunks; ++c) _mm_store_si128((__m128i *)(w.in + c), stamp);
+    for (size_t c = 0; c < nchunks; ++c) _mm_store_si128((__m128i *)(w.in + c), w.vram ? vstamp : stamp);
     if (total > head) explicit_bzero(w.tail, total - head);
+    if (w.vram) _mm_sfence();
     explicit_bzero(w.out, len + 16);
     const uint64_t h4 = host_ns();
     t_host[0] = h1 - h0; t_host[1] = h2 - h0; t_host[2] = h3 - h0; t_host[3] = h4 - h0;
