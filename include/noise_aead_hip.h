@@ -389,8 +389,12 @@ void noise_aead_debug_worker_stamps(uint32_t *out, int n);
  *   compute phase (s_memtime cycles / s_memrealtime time), 0 if none. */
 double noise_aead_debug_worker_clock_mhz(void);
 /* noise_aead_debug_worker_fast_stamps: shader-cycle stamps through the
- *   worker's latency-first ChaChaPoly path (n <= 8). */
+ *   worker's latency-first ChaChaPoly path, or its AES-GCM record (n <= 8). */
 void noise_aead_debug_worker_fast_stamps(uint32_t *out, int n);
+/* noise_aead_debug_worker_placement: where the current device's worker
+ *   takes requests: 0 not started, 1 pinned host memory, 2 device memory
+ *   written through the BAR (large-BAR devices, NOISE_AEAD_WORKER_VRAM). */
+int noise_aead_debug_worker_placement(void);
 /* noise_aead_debug_worker_host_ns: the calling thread's last worker call on
  *   the host, ns from its start: packed, doorbell, done seen, returned. */
 void noise_aead_debug_worker_host_ns(uint64_t *out, int n);

@@ -108,6 +108,8 @@ void noise_aead_debug_worker_stamps(uint32_t *out, int n)
 
 double noise_aead_debug_worker_clock_mhz(void) { return 0.0; }
 
+int noise_aead_debug_worker_placement(void) { return 0; }
+
 void noise_aead_debug_worker_fast_stamps(uint32_t *out, int n)
 {
     for (int i = 0; i < n; ++i) out[i] = 0;

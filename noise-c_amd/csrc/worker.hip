@@ -875,6 +875,16 @@ extern "C" void noise_aead_debug_worker_fast_stamps(uint32_t *out, int n)
     for (int i = 0; i < n && i < 8; ++i) out[i] = s ? s->fstamps[i] : 0;
 }
 
+/* Test hook: 0 no worker set up on this device, 1 requests in pinned host
+   memory, 2 in device memory. */
+extern "C" int noise_aead_debug_worker_placement(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+    const Worker &w = g_worker[dev];
+    return w.state != 1 ? 0 : (w.vram ? 2 : 1);
+}
+
 /* Test hook: the shader clock (MHz) of the last worker request's compute
    phase (s_memtime cycles over s_memrealtime time). */
 extern "C" double noise_aead_debug_worker_clock_mhz(void)

@@ -10,7 +10,10 @@ src/backend/ref/cipher-chachapoly.c:107-143 and cipher-aesgcm.c:156-188),
 then opened back, then opened tampered: MAC failure, buffer and nonce left
 as given (cipherstate.c:373-410).
 """
+import os
 import random
+import subprocess
+import sys
 
 import pytest
 
@@ -63,8 +66,24 @@ def test_worker_single_records_vs_oracle(aead, gpu, oracle, cipher):
         assert rc == 0 and back == pt, (L, A)
         n += 1
         assert tx.nonce == n and rx.nonce == n
+    # requests go to device memory on a large-BAR device, else host memory
+    assert aead.lib().noise_aead_debug_worker_placement() in (1, 2)
     tx.free()
     rx.free()
+
+
+@pytest.mark.parametrize("vram", ["0", "1"])
+def test_worker_request_placement(aead, gpu, vram):
+    """Both request placements: pinned host memory with
+    12-byte chunks, and device memory written through the BAR with 8-byte
+    stamped halves.  The placement is chosen once per process, so each runs
+    in one child process (worker_mode_check.py) against the oracle."""
+    env = dict(os.environ, NOISE_AEAD_WORKER_VRAM=vram)
+    r = subprocess.run([sys.executable, "-u", os.path.join(os.path.dirname(__file__), "worker_mode_check.py")],
+                       env=env, timeout=110, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    placement = int(r.stdout.split("placement")[-1].split()[0])
+    assert placement == 1 if vram == "0" else placement in (1, 2)
 
 
 def test_worker_in_place_buffer_semantics(aead, gpu, oracle):

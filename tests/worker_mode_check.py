@@ -1,0 +1,59 @@
+"""Child process of test_gpu_worker.py's placement test (not collected by
+pytest): single-record seal/open through the resident worker, checked
+against the oracle, under whatever NOISE_AEAD_WORKER_VRAM the parent set.
+The worker picks its request placement once per process, hence the child.
+Prints "placement N" (noise_aead_debug_worker_placement) and exits non-zero
+on the first mismatch."""
+import os
+import random
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "noise-c_amd")):
+    sys.path.insert(0, p)
+
+import noise_aead as aead  # noqa: E402
+import oracle as O  # noqa: E402
+
+
+def main():
+    if not os.path.exists(O.ORACLE_SO):
+        O.build(ref=False)
+    orc = O.Oracle()
+    aead.lib()
+    for cipher in (0x4301, 0x4302):
+        rnd = random.Random(cipher ^ 0x77)
+        key = bytes(rnd.randrange(256) for _ in range(32))
+        _, tx = aead.CipherState.new_by_id(cipher)
+        _, rx = aead.CipherState.new_by_id(cipher)
+        assert tx.init_key(key) == 0 and rx.init_key(key) == 0
+        n = 0
+        for L in (0, 1, 17, 1024, 1400, 2100, 3100, 4033, 8000, 16384):
+            if cipher == 0x4302 and L > 4096:
+                continue
+            for A in (0, 32):
+                pt = bytes(rnd.randrange(256) for _ in range(L))
+                ad = bytes(rnd.randrange(256) for _ in range(A))
+                ct = tx.seal(pt, ad)
+                if ct != orc.encrypt(cipher, key, n, pt, ad):
+                    print("seal mismatch", hex(cipher), L, A)
+                    return 1
+                bad = bytearray(ct)
+                bad[rnd.randrange(len(bad))] ^= 1
+                rc, back = rx.open(bytes(bad), ad)
+                if rc != aead.ERROR_MAC_FAILURE or back != bytes(bad) or rx.nonce != n:
+                    print("tamper not rejected", hex(cipher), L, A)
+                    return 1
+                rc, back = rx.open(ct, ad)
+                if rc != 0 or back != pt:
+                    print("open mismatch", hex(cipher), L, A)
+                    return 1
+                n += 1
+        tx.free()
+        rx.free()
+    print("placement", aead.lib().noise_aead_debug_worker_placement())
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
