@@ -400,7 +400,11 @@ int noise_aead_debug_worker_placement(void);
 void noise_aead_debug_worker_host_ns(uint64_t *out, int n);
 void *noise_aead_debug_last_freed_ctx(size_t *bytes);
 
-/* Default lanes per record the library picks for a batch of n records. */
+/* Default lanes per record the library picks for a uniform batch of n
+ * records in a FAST layout (16-B aligned slots readable up to roundup64(len)):
+ * ChaChaPoly 1 from 64 Ki records on (one lane per record, LDS-staged), else
+ * 4 or 8, and up to 64 for batches of at most 512 records; AES-GCM 4.  Other
+ * layouts, VERIFY_FIRST opens and ragged batches keep the multi-lane rule. */
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records);
 
 /* Deterministic synthetic bytes (bench/test input): 64-bit LE word w of the

@@ -56,6 +56,34 @@ bool uniform_fast(const NoiseAeadUniform *j, bool open)
     return true;
 }
 
+bool verify_first(const NoiseAeadUniform *j, bool open);
+
+/* One lane per record (chachapoly.hip seal_solo_staged) for uniform FAST
+   batches from SOLO_MIN_RECORDS on: one Poly1305 chain per record with the
+   clamped r, the per-record work paid once per 64 records; C2 +8-9 %, C4
+   +13 % over four lanes (profiles/r04/solo_ab.jsonl).  Below that the
+   batch is under one wave per SIMD at one lane.  NOISE_AEAD_SOLO=0 keeps
+   the 4-lane kernels (A/B runs). */
+constexpr uint32_t SOLO_MIN_RECORDS = 65536;
+
+bool solo_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("NOISE_AEAD_SOLO");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+int uniform_lanes(const NoiseAeadUniform *j, bool open)
+{
+    if (j->lanes_per_record) return (int)j->lanes_per_record;
+    if (j->n_records >= SOLO_MIN_RECORDS && solo_enabled() && uniform_fast(j, open) &&
+        !verify_first(j, open))
+        return 1;
+    return auto_lanes(j->n_records, 0);
+}
+
 void job_span(const NoiseAeadUniform *j, bool out, bool open, uint64_t &lo, uint64_t &hi);
 
 /* open = the job is an open (its input holds CT || tag).  In-place jobs must
@@ -123,8 +151,8 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     UniformArgs a = to_args(job);
     a.vf = verify_first(job, open);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
-        int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
-        const bool ukey = k >= 4 && job->recs_per_state % (64u / (uint32_t)k) == 0;
+        const int k = uniform_lanes(job, open);
+        const bool ukey = (k >= 4 || k == 1) && job->recs_per_state % (64u / (uint32_t)k) == 0;
         /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC): open
            balances its waves' progress (profiles/r01_prio_ab.jsonl); in the
            seal it measured neutral (profiles/r02/timeline_c2_seal_open_duplex.log) */
@@ -221,11 +249,10 @@ int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform
         return rc;
     }
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY && sj->n_records && oj->n_records) {
-        const int ks = sj->lanes_per_record ? (int)sj->lanes_per_record : auto_lanes(sj->n_records, 0);
-        const int ko = oj->lanes_per_record ? (int)oj->lanes_per_record : auto_lanes(oj->n_records, 0);
-        const bool us = ks >= 4 && sj->recs_per_state % (64u / (uint32_t)ks) == 0;
-        const bool uo = ko >= 4 && oj->recs_per_state % (64u / (uint32_t)ko) == 0;
-        if (ks == ko && (ks == 4 || ks == 8) && us == uo && uniform_fast(sj, false) &&
+        const int ks = uniform_lanes(sj, false), ko = uniform_lanes(oj, true);
+        const bool us = (ks >= 4 || ks == 1) && sj->recs_per_state % (64u / (uint32_t)ks) == 0;
+        const bool uo = (ko >= 4 || ko == 1) && oj->recs_per_state % (64u / (uint32_t)ko) == 0;
+        if (ks == ko && (ks == 1 || ks == 4 || ks == 8) && us == uo && uniform_fast(sj, false) &&
             uniform_fast(oj, true)) {
             return chacha_duplex(to_args(sj), to_args(oj), ks, us, (hipStream_t)stream);
         }
@@ -492,7 +519,8 @@ int noise_aead_dev_pad(NoiseRandSnapshot *d_rand, uint8_t *d_payloads, uint64_t 
 
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)
 {
-    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) return auto_lanes(n_records, 0);
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY)
+        return n_records >= SOLO_MIN_RECORDS && solo_enabled() ? 1 : auto_lanes(n_records, 0);
     if (cipher_id == NOISE_CIPHER_AESGCM) return GCM_LANES;
     return 0;
 }

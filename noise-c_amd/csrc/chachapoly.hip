@@ -1112,6 +1112,298 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
     }
 }
 
+/* ---------------- one lane per record, LDS-staged (uniform FAST batches)
+ *
+ * Round 4.  Every lane owns a whole record: its ChaCha blocks 0..J in order
+ * and ONE Poly1305 Horner chain over the record's blocks with the clamped r
+ * itself, so every Poly block is a radix-2^32 p32_block (20 v_mad_u64_u32, no
+ * limb split) and there is no r^(4K-3) jump, no per-lane power of r and no
+ * group sum — the per-record work of the 4-lane kernels (powers, group sum,
+ * tag) is paid once per 64 records instead of once per 16.  Per 1400-B
+ * record: 23 ChaCha blocks (no end-alignment slot) + 89 p32 blocks.
+ *
+ * A step moves two units (128 B, one whole line of the 128-B record slots)
+ * of all 64 records of the wave through an 8 KB LDS tile, double-buffered:
+ * LDS-DMA instruction i (0..7) fills slots 64i..64i+63 with the 128-B runs
+ * of records 8i..8i+7, so every instruction covers eight whole lines, and
+ * the stores leave the same way.  Owner L's chunk c (0..7) sits in slot
+ * 8L + (c ^ (L & 7)): the XOR makes the owner-side ds_*_b128 (lanes 8 apart
+ * in the same chunk) bank-conflict-free.  16 KB of LDS per wave caps a CU at
+ * 8 waves (two per SIMD), which is all a VALU-bound wave needs: one wave
+ * issues the ChaCha stream at ~4.15 cycles per instruction on its own
+ * (DESIGN §5), and the 64 Ki records of C2 are 1024 waves per job.
+ */
+constexpr uint32_t SOLO_TILE = 512; /* uint4 slots per tile: 64 owners x 8 chunks */
+
+NA_DEV void p32_ad(P32 &acc, const R32 &r, const uint8_t *ad, uint32_t ad_len);
+NA_DEV void p32_unit(P32 &acc, const R32 &r, const uint32_t c[16], uint32_t nb);
+
+NA_DEV uint32_t solo_slot(uint32_t L, uint32_t c) { return L * 8 + (c ^ (L & 7)); }
+
+/* chunk this lane moves in a coalesced instruction (slot 64i + lane holds
+   owner 8i + lane/8, chunk (lane ^ lane/8) & 7) */
+NA_DEV uint32_t solo_chunk(uint32_t lane) { return (lane ^ (lane >> 3)) & 7; }
+
+/* One LDS-DMA instruction (global_load_lds_dwordx4: lane l's 16 bytes land
+   at LDS address lds + 16 l), written as inline asm so that hipcc does not
+   see an LDS write: it would otherwise wait for the youngest such DMA before
+   every later LDS access of the wave (tile reads AND writes), i.e. for the
+   next step's DMA right after issuing it.  The one-lane kernels place their
+   own s_waitcnt vmcnt(0) instead (solo_wait).  m0 carries the LDS address; no
+   other code of these kernels keeps a value in m0 across the asm. */
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+NA_DEV void dma16_asm(const void *g, uint32_t lds)
+{
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(g), "s"(lds) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+/* every vector-memory operation of the wave done (the DMA into the tile
+   about to be read, issued a step earlier, and the stores issued with it) */
+NA_DEV void solo_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+/* DMA of step m (units 2m, 2m+1) of the wave's records into tile t.  Chunks
+   at or past lim (= 64 J, the end of the record's last unit) re-read the
+   step's first unit instead: FAST slots are only readable up to
+   roundup64(len). */
+NA_DEV void solo_dma(const UniformArgs &a, uint32_t rec0, uint32_t lane, uint32_t m,
+                     uint32_t lim, uint4 *t)
+{
+    const uint32_t c = solo_chunk(lane);
+    uint32_t off = 128u * m + 16u * c;
+    if (off >= lim) off -= 64u;
+    const uint32_t last = a.n_records - 1;
+    const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        dma16_asm((const void *)(a.in + (size_t)min(rec0 + 8u * i + (lane >> 3), last) * a.in_stride + off),
+                  base + 1024u * (uint32_t)i);
+}
+
+/* coalesced stores of step m's chunks below full_lim (the full units before
+   the record's last one; the owner stores that one exactly); okm bit i gates
+   instruction i */
+NA_DEV void solo_store(const UniformArgs &a, uint32_t rec0, uint32_t lane, uint32_t m,
+                       uint32_t full_lim, const uint4 *t, uint32_t okm)
+{
+    const uint32_t off = 128u * m + 16u * solo_chunk(lane);
+    if (off + 16u > full_lim) return;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint4 q = t[64 * i + lane];
+        const uint32_t r = rec0 + 8u * i + (lane >> 3);
+        if (r < a.n_records && ((okm >> i) & 1)) rec_store16(a.out + (size_t)r * a.out_stride + off, q);
+    }
+}
+
+NA_DEV void solo_get(const uint4 *t, uint32_t L, uint32_t u, uint32_t w[16])
+{
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) {
+        const uint4 v = t[solo_slot(L, 4 * u + c)];
+        w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+    }
+}
+
+NA_DEV void solo_put(uint4 *t, uint32_t L, uint32_t u, const uint32_t w[16])
+{
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c)
+        t[solo_slot(L, 4 * u + c)] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+}
+
+/* Poly key block 0: r (clamped, radix 2^32), s; AD absorbed. */
+NA_DEV void solo_poly_key(const uint32_t key[8], const ChaPre &pre, uint32_t n_lo, uint32_t n_hi,
+                          const uint8_t *ad, uint32_t ad_len, R32 &r, uint32_t s[4], P32 &h)
+{
+    uint32_t x[16];
+    chacha20_block_pre(key, pre, 0u, n_lo, n_hi, x);
+    r = r32_from_key(x[0], x[1], x[2], x[3]);
+    s[0] = x[4]; s[1] = x[5]; s[2] = x[6]; s[3] = x[7];
+    h = p32_zero();
+    if (ad_len) p32_ad(h, r, ad, ad_len);
+}
+
+NA_DEV void solo_tag(P32 h, const R32 &r, uint32_t ad_len, uint32_t len, const uint32_t s[4],
+                     uint32_t tag[4])
+{
+    p32_block(h, r, ad_len, 0u, len, 0u);
+    fe_finish(p32_to_fe(h), s, tag);
+}
+
+/* Per-lane view of a wave's 64 records in the one-lane kernels. */
+struct SoloRec {
+    uint32_t lane, rec0, rec_raw, rc, len, J, S, lim, full_lim, tail;
+    bool live;
+};
+
+NA_DEV SoloRec solo_rec(const UniformArgs &a, uint32_t wave_job)
+{
+    SoloRec q;
+    q.lane = threadIdx.x & 63;
+    q.rec0 = wave_job * 64u;
+    q.rec_raw = q.rec0 + q.lane;
+    q.live = q.rec_raw < a.n_records;
+    q.rc = q.live ? q.rec_raw : a.n_records - 1;
+    q.len = a.len;
+    q.J = (q.len + 63) / 64;
+    q.S = (q.J + 1) / 2;
+    q.lim = 64u * q.J;
+    q.full_lim = q.J ? 64u * (q.J - 1) : 0u; /* the full units before the last */
+    q.tail = q.len - q.full_lim;             /* bytes of unit J-1 */
+    return q;
+}
+
+/* The one pass over a wave's records (seal: plaintext -> CT; open: CT ->
+   plaintext, Poly1305 over the CT as read), leaving the Horner value in h.
+   Order inside step m, chosen so that every wait for memory is for work
+   issued a whole step earlier:
+     wait   -- DMA(m), issued during step m-1, and the stores of step m-2
+     read   -- step m's two units, tile m&1 -> registers
+     store  -- step m-1's output, still in the other tile, leaves
+     DMA    -- step m+1's units into that other tile
+     compute-- two ChaCha blocks, Poly1305, output into tile m&1
+   (hipcc waits before an LDS read for the youngest LDS-DMA; reading the tile
+   after issuing the next DMA, as the 4-lane kernels do, made every step wait
+   for the DMA it had just issued and serialised the stores behind it.) */
+template <bool OPEN>
+NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const uint32_t key[8],
+                      const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, const R32 &r, P32 &h)
+{
+    for (uint32_t m = 0; m < q.S; ++m) {
+        uint4 *cur = tiles + SOLO_TILE * (m & 1), *nxt = tiles + SOLO_TILE * ((m + 1) & 1);
+        uint32_t wu[2][16];
+        solo_wait();
+        solo_get(cur, q.lane, 0, wu[0]);
+        solo_get(cur, q.lane, 1, wu[1]);
+        if (m >= 1) solo_store(a, q.rec0, q.lane, m - 1, q.full_lim, nxt, 0xffu);
+        __builtin_amdgcn_wave_barrier();
+        if (m + 1 < q.S) solo_dma(a, q.rec0, q.lane, m + 1, q.lim, nxt);
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t j = 2 * m + u; /* unit, ChaCha block j + 1 */
+            if (j < q.J) {
+                uint32_t x[16], w[16];
+                chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+                uint32_t nb = 4;
+                if constexpr (OPEN) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] = wu[u][i];
+                    if (j == q.J - 1) { /* bytes past len are never stored */
+                        mask_unit(w, q.tail);
+                        nb = (q.tail + 15) / 16;
+                    }
+                    p32_unit(h, r, w, nb);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+                    if (j == q.J - 1 && q.live) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] = wu[u][i] ^ x[i];
+                    if (j == q.J - 1) {
+                        if (q.live) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
+                        mask_unit(w, q.tail);
+                        nb = (q.tail + 15) / 16;
+                    }
+                    p32_unit(h, r, w, nb);
+                }
+                solo_put(cur, q.lane, u, w);
+            }
+        }
+    }
+    if (q.S) {
+        __builtin_amdgcn_wave_barrier();
+        solo_store(a, q.rec0, q.lane, q.S - 1, q.full_lim, tiles + SOLO_TILE * ((q.S - 1) & 1), 0xffu);
+    }
+}
+
+template <bool UKEY>
+NA_DEV void seal_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_job)
+{
+    const SoloRec q = solo_rec(a, wave_job);
+    uint32_t key[8], n_lo, n_hi;
+    u_key_nonce<UKEY>(a, q.rec0, q.rc, key, n_lo, n_hi);
+    ChaPre pre;
+    chacha_pre(key, n_lo, n_hi, pre);
+    if (q.S) solo_dma(a, q.rec0, q.lane, 0, q.lim, tiles);
+    R32 r;
+    uint32_t s[4];
+    P32 h;
+    solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, q.rc) : nullptr, a.ad_len, r, s, h);
+    solo_pass<false>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
+    uint32_t tag[4];
+    solo_tag(h, r, a.ad_len, q.len, s, tag);
+    if (q.live) tag_out(u_dst(a, q.rc) + q.len, q.len, tag);
+}
+
+/* Open, one pass: Poly1305 over each ciphertext unit as it arrives, then
+   the plaintext out; a wave holding a rejected record repairs it after the
+   verdict exactly as open_il_staged does (in place: XOR with the key stream
+   once more; out of place: zeroed). */
+template <bool UKEY>
+NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_job)
+{
+    const SoloRec q = solo_rec(a, wave_job);
+    const uint32_t lane = q.lane, rec0 = q.rec0, rec_raw = q.rec_raw, rc = q.rc, len = q.len;
+    const uint32_t J = q.J, S = q.S, lim = q.lim, full_lim = q.full_lim, tail = q.tail;
+    const bool live = q.live;
+    uint32_t key[8], n_lo, n_hi;
+    u_key_nonce<UKEY>(a, rec0, rc, key, n_lo, n_hi);
+    ChaPre pre;
+    chacha_pre(key, n_lo, n_hi, pre);
+    if (S) solo_dma(a, rec0, lane, 0, lim, tiles);
+    R32 r;
+    uint32_t s[4];
+    P32 h;
+    solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, rc) : nullptr, a.ad_len, r, s, h);
+    solo_pass<true>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
+    uint32_t tag[4], got[4];
+    solo_tag(h, r, a.ad_len, len, s, tag);
+    tag_in<true>(u_src(a, rc), len, got); /* the tag bytes are never written */
+    const bool ok = tag_equal(tag, got);
+    if (live && a.status) a.status[rec_raw] = ok ? 0 : 1;
+    const bool bad = live && !ok;
+    if (__ballot(bad) == 0) return; /* wave-uniform: the common case */
+
+    /* repair pass: bit i of badm = the owner coalesced instruction i serves */
+    uint32_t badm = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        badm |= (__shfl((int)bad, (int)(8u * i + (lane >> 3)), 64) != 0 ? 1u : 0u) << i;
+    const bool inplace = a.in == a.out && a.in_stride == a.out_stride;
+    __threadfence(); /* this wave's plaintext stores, visible to its reads below */
+    for (uint32_t m = 0; m < S; ++m) {
+        __builtin_amdgcn_wave_barrier();
+        if (inplace) solo_dma(a, rec0, lane, m, lim, tiles);
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t j = 2 * m + u;
+            if (j < J) {
+                uint32_t w[16];
+                if (inplace) {
+                    uint32_t x[16];
+                    chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_wave_barrier();
+                    solo_get(tiles, lane, u, w);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] = 0;
+                }
+                if (j == J - 1 && bad) last_unit_out(u_dst(a, rc) + full_lim, tail, w);
+                __builtin_amdgcn_wave_barrier();
+                solo_put(tiles, lane, u, w);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        solo_store(a, rec0, lane, m, full_lim, tiles, badm);
+    }
+}
+
 /* ------------------------------------------------- contiguous (K = 1, 2) */
 
 NA_DEV void p32_ad(P32 &acc, const R32 &r, const uint8_t *ad, uint32_t ad_len)
@@ -1443,6 +1735,44 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_persist(
             atomicExch(&ctr[1], 0u);
         }
     }
+}
+
+/* One lane per record (seal_solo_staged): two waves per SIMD, 16 KB of LDS
+   each; 256 records per workgroup. */
+#define NA_SOLO_OCC __attribute__((amdgpu_waves_per_eu(2)))
+
+template <bool UKEY>
+__global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seal_solo(UniformArgs a)
+{
+    __shared__ uint4 tiles[4][2 * SOLO_TILE];
+    seal_solo_staged<UKEY>(a, tiles[threadIdx.x >> 6], wave_of(blockIdx.x));
+}
+
+template <bool UKEY>
+__global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_open_solo(UniformArgs a)
+{
+    __shared__ uint4 tiles[4][2 * SOLO_TILE];
+    open_solo_staged<UKEY>(a, tiles[threadIdx.x >> 6], wave_of(blockIdx.x));
+}
+
+/* chachapoly_duplex_staged's two-job launch over the one-lane kernels */
+template <bool UKEY>
+__global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_duplex_solo(
+    UniformArgs s, UniformArgs o, uint32_t s_blocks, uint32_t o_blocks)
+{
+    __shared__ uint4 tiles[4][2 * SOLO_TILE];
+    const uint32_t n = min(s_blocks, o_blocks);
+    uint32_t b = blockIdx.x;
+    bool open;
+    if (b < 2 * n) {
+        open = b & 1;
+        b >>= 1;
+    } else {
+        open = o_blocks > s_blocks;
+        b -= n;
+    }
+    if (open) open_solo_staged<UKEY>(o, tiles[threadIdx.x >> 6], wave_of(b));
+    else seal_solo_staged<UKEY>(s, tiles[threadIdx.x >> 6], wave_of(b));
 }
 
 template <int K, bool FAST>

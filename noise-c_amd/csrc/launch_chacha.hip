@@ -40,7 +40,13 @@ template <bool FAST>
 KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf)
 {
     switch (k) {
-    case 1: return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
+    case 1:
+        /* one lane per record, LDS-staged (seal_solo_staged) */
+        if (FAST && !(open && vf)) {
+            if (ukey) return open ? chachapoly_open_solo<true> : chachapoly_seal_solo<true>;
+            return open ? chachapoly_open_solo<false> : chachapoly_seal_solo<false>;
+        }
+        return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
     case 2: return open ? chachapoly_open_uniform<2, FAST> : chachapoly_seal_uniform<2, FAST>;
     case 4:
         if (FAST && !(open && vf)) return chacha_staged_fn<4>(open, ukey);
@@ -163,7 +169,8 @@ int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, 
     const uint32_t sb = (uint32_t)(((uint64_t)a.n_records * k + 255) / 256);
     const uint32_t ob = (uint32_t)(((uint64_t)b.n_records * k + 255) / 256);
     void (*fn)(UniformArgs, UniformArgs, uint32_t, uint32_t);
-    if (k == 4) fn = ukey ? chachapoly_duplex_staged<4, true> : chachapoly_duplex_staged<4, false>;
+    if (k == 1) fn = ukey ? chachapoly_duplex_solo<true> : chachapoly_duplex_solo<false>;
+    else if (k == 4) fn = ukey ? chachapoly_duplex_staged<4, true> : chachapoly_duplex_staged<4, false>;
     else if (k == 8) fn = ukey ? chachapoly_duplex_staged<8, true> : chachapoly_duplex_staged<8, false>;
     else return NOISE_ERROR_INVALID_PARAM;
     hipLaunchKernelGGL(fn, dim3(sb + ob), dim3(256), 0, s, a, b, sb, ob);

@@ -181,12 +181,13 @@ def test_batch_host_rules(aead_built):
 
 
 def test_default_lane_policy(aead_built):
-    """Lanes per record the library picks (aead_api.hip auto_lanes): 4 at the
-    BASELINE sizes, 8 below 64 Ki records, and wide groups (up to a wave per
+    """Lanes per record the library picks (aead_api.hip uniform_lanes /
+    auto_lanes): one lane per record at the BASELINE sizes (64 Ki records and
+    up, FAST layouts), 8 below 64 Ki records, and wide groups (up to a wave per
     record) only for batches of at most 512 records — the latency regime."""
     A = aead_built
     lanes = lambda n: A.dev_default_lanes(A.CHACHAPOLY, n)
-    assert lanes(65536) == 4 and lanes(1 << 20) == 4
+    assert lanes(65536) == 1 and lanes(1 << 20) == 1
     assert lanes(65535) == 8 and lanes(513) == 8
     assert lanes(512) == 64 and lanes(1) == 64
     assert A.dev_default_lanes(A.AESGCM, 1) == 4

@@ -77,37 +77,60 @@ def test_full_config_digest_on_gpu(name):
     assert hashlib.sha256(opened.tobytes()).hexdigest() == c["pt_sha256"], name
 
 
+def _shard_golden():
+    with open(os.path.join(ROOT, "tests", "golden", "shard_digests.json")) as f:
+        return json.load(f)["configs"]
+
+
+def _mask_t(off, lens, buf):
+    """Mask of the bytes [off_i, off_i + lens_i) of every record of buf, built
+    on the GPU (a +1/-1 boundary cumsum); records are in offset order, so
+    buf[mask] is the records' bytes packed in record order."""
+    import torch
+    edge = torch.zeros(buf.numel() + 1, dtype=torch.int32, device=buf.device)
+    o = torch.from_numpy(off).to(buf.device)
+    e = o + torch.from_numpy(lens).to(buf.device)
+    edge.index_add_(0, o, torch.ones_like(o, dtype=torch.int32))
+    edge.index_add_(0, e, -torch.ones_like(e, dtype=torch.int32))
+    return torch.cumsum(edge[:-1], 0) > 0
+
+
 @pytest.mark.gpu
-def test_full_c5_digest_on_gpu():
-    """C5 at N = 1 (bench.py run_mixed, rank 0): the mixed ChaChaPoly/AES-GCM
-    ragged batch, 128 Ki records of 64 B-16 KiB over 512 states, sealed with
-    the FAST ragged kernels; every record's ct || tag, in record order, hashes
-    to the digest of the reference build, and the open accepts them all and
-    restores every plaintext."""
+@pytest.mark.parametrize("rank", range(8))
+def test_c5_shard_digest_on_gpu(rank):
+    """C5 rank by rank (bench.py run_mixed at rank r of the 8-GPU job, laid
+    out on this one GPU): the mixed ChaChaPoly/AES-GCM ragged batch of rank
+    r — 128 Ki records of 64 B-16 KiB over its 512 states, its own length
+    mix, nonces, key ids and state parities — sealed with the FAST ragged
+    kernels; every record's ct || tag, in record order, hashes to the digest
+    of the reference build for that rank (tests/golden/shard_digests.json;
+    rank 0 is also config_digests.json's), and the open accepts every record
+    and restores every plaintext."""
     import torch
 
     import noise_aead as A
     from bench import CHACHA, AES, CONFIGS as BC, mixed_layout
     A.lib()
-    c = _golden()["c5"]
+    want = _shard_golden()["c5"]["rank_sealed_sha256"][rank]
     R, S = BC["c5"]["records"], BC["c5"]["states"]
-    assert (R, S) == (c["records"], c["states"])
-    lay = mixed_layout(R, S, 0)
-    assert lay["total"] == c["total"] and int(lay["lens"].sum()) == c["lens_sum"]
+    if rank == 0:
+        c = _golden()["c5"]
+        assert (R, S) == (c["records"], c["states"]) and want == c["sealed_sha256"]
+    lay = mixed_layout(R, S, rank)
     sp = torch.cuda.current_stream().cuda_stream
     rec_dt = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "<u8"),
                        ("ad_off", "<u8"), ("len", "<u4"), ("ad_len", "<u4")])
     pt = torch.empty(lay["total"], dtype=torch.uint8, device="cuda")
-    assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), SEED_PT, 0, sp) == 0
+    assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), SEED_PT, rank << 40, sp) == 0
     ct = torch.zeros_like(pt)
     back = torch.zeros_like(pt)
     groups = []
     for cipher, parity in ((CHACHA, 0), (AES, 1)):
-        states = [s for s in range(S) if s % 2 == parity]
+        states = [s for s in range(S) if (rank * S + s) % 2 == parity]
         cb = A.dev_ctx_bytes(cipher)
         raw = torch.empty(len(states) * 32, dtype=torch.uint8, device="cuda")
         for i, s in enumerate(states):
-            assert A.dev_fill_splitmix(raw[32 * i:].data_ptr(), 32, SEED_KEY, 4 * s, sp) == 0
+            assert A.dev_fill_splitmix(raw[32 * i:].data_ptr(), 32, SEED_KEY, 4 * (rank * S + s), sp) == 0
         ctx = torch.empty(len(states) * cb, dtype=torch.uint8, device="cuda")
         assert A.dev_prepare(cipher, raw.data_ptr(), len(states), ctx.data_ptr(), sp) == 0
         slot_of = {s: i for i, s in enumerate(states)}
@@ -130,24 +153,22 @@ def test_full_c5_digest_on_gpu():
     torch.cuda.synchronize()
     for g in groups:
         assert int(g[4].max().item()) == 0
-    ct_h, back_h, pt_h = ct.cpu().numpy(), back.cpu().numpy(), pt.cpu().numpy()
-    hs, hb, hp = hashlib.sha256(), hashlib.sha256(), hashlib.sha256()
-    for off, L in zip(lay["off"].tolist(), lay["lens"].tolist()):
-        hs.update(ct_h[off:off + L + 16])
-        hb.update(back_h[off:off + L])
-        hp.update(pt_h[off:off + L])
-    assert hp.hexdigest() == c["pt_sha256"]
-    assert hs.hexdigest() == c["sealed_sha256"]
-    assert hb.hexdigest() == c["pt_sha256"]
+    off, lens = lay["off"].astype(np.int64), lay["lens"].astype(np.int64)
+    sealed = ct[_mask_t(off, lens + 16, ct)].cpu().numpy()
+    assert hashlib.sha256(sealed.tobytes()).hexdigest() == want, rank
+    del sealed
+    m = _mask_t(off, lens, pt)
+    assert torch.equal(back[m], pt[m])
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["c2", "c3"])
-def test_full_size_duplex_at_bench_slots(name):
+@pytest.mark.parametrize("name,lanes", [("c2", 0), ("c2", 4), ("c3", 0)])
+def test_full_size_duplex_at_bench_slots(name, lanes):
     """The kernels bench.py times: C2 / C3 at full size
     through noise_aead_dev_duplex_uniform at the bench's 128-B record slots
     (in_stride 1408, out_stride 1536), one state, recs_per_state 65 536 —
-    chachapoly_duplex_staged<4, true> / gcm_duplex_fused<false>.  The seal
+    chachapoly_duplex_solo<true> (the default: one lane per record; lanes=4
+    the four-lane chachapoly_duplex_staged<4, true>) / gcm_duplex_fused<false>.  The seal
     half's sealed records hash to the golden digest (cipher-chachapoly.c
     :107-133 / cipher-aesgcm.c:156-170 bytes); the open half, over a batch
     sealed beforehand with 64 records tampered, accepts every other record
@@ -170,7 +191,7 @@ def test_full_size_duplex_at_bench_slots(name):
     assert hashlib.sha256(pt.view(N, ins)[:, :L].contiguous().cpu().numpy().tobytes()).hexdigest() \
         == c["pt_sha256"]
     common = dict(ctx=ctx.data_ptr(), nonce_base=nb.data_ptr(), length=L, n_records=N,
-                  recs_per_state=N)
+                  recs_per_state=N, lanes=lanes)
     # batch B: sealed by the separate kernel, then tampered
     ct_b = torch.empty(N * outs, dtype=torch.uint8, device="cuda")
     assert A.dev_uniform(False, cipher, inp=pt.data_ptr(), out=ct_b.data_ptr(), in_stride=ins,

@@ -146,12 +146,13 @@ def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed, r
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L])
 
 
-@pytest.mark.parametrize("cipher", [CHACHA, AES])
-def test_uniform_staged_kernels(aead, gpu, oracle, cipher):
+@pytest.mark.parametrize("cipher,lanes", [(CHACHA, 0), (CHACHA, 1), (CHACHA, 4), (AES, 0)])
+def test_uniform_staged_kernels(aead, gpu, oracle, cipher, lanes):
     """FAST layouts with one state per 256 records: the LDS-staged kernels
-    (ChaChaPoly wave-uniform key, AESGCM replicated T-tables) on a batch whose
-    last workgroup is partial, every record vs the oracle, with AD."""
-    rng = np.random.default_rng(4242 + (cipher & 3))
+    (ChaChaPoly wave-uniform key at one and four lanes per record, AESGCM
+    replicated T-tables) on a batch whose last workgroup is partial, every
+    record vs the oracle, with AD."""
+    rng = np.random.default_rng(4242 + (cipher & 3) + 100 * lanes)
     rps, count = 256, 600
     S = (count + rps - 1) // rps
     for L, adl in [(0, 0), (1, 0), (15, 0), (16, 0), (17, 0), (100, 0), (1400, 0), (1401, 0),
@@ -166,14 +167,14 @@ def test_uniform_staged_kernels(aead, gpu, oracle, cipher):
         exp = oracle_seal_records(oracle, cipher, keys, nb, rps, pt, in_stride, L, count,
                                   out_stride, **kw)
         got, _ = gpu_uniform(aead, False, cipher, keys, nb, rps, pt, in_stride, L, count,
-                             out_stride, **kw)
+                             out_stride, lanes=lanes, **kw)
         assert np.array_equal(got[:count * out_stride], exp[:count * out_stride]), f"len={L} ad={adl}"
         ct = got.copy()
         bad = sorted(set(int(x) for x in rng.integers(0, count, 7)))
         for b in bad:
             ct[b * out_stride + int(rng.integers(0, L + 16))] ^= 0x80
         back, st = gpu_uniform(aead, True, cipher, keys, nb, rps, ct, out_stride, L, count,
-                               in_stride, out_init=0x3C, **kw)
+                               in_stride, out_init=0x3C, lanes=lanes, **kw)
         for i in range(count):
             seg = back[i * in_stride: i * in_stride + L]
             if i in bad:
@@ -185,7 +186,8 @@ def test_uniform_staged_kernels(aead, gpu, oracle, cipher):
 
 @pytest.mark.parametrize("cipher,lanes,rps,adl", [(CHACHA, 4, 256, 0), (CHACHA, 4, 13, 0),
                                                   (CHACHA, 8, 256, 0), (CHACHA, 8, 13, 0),
-                                                  (CHACHA, 1, 16, 0), (AES, 0, 256, 0),
+                                                  (CHACHA, 1, 16, 0), (CHACHA, 1, 256, 0),
+                                                  (CHACHA, 1, 64, 21), (AES, 0, 256, 0),
                                                   (AES, 0, 13, 0), (CHACHA, 4, 256, 21),
                                                   (AES, 0, 256, 21)])
 def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes, rps, adl):
@@ -240,6 +242,7 @@ SLOT_CASES = [((1400, 1024, 512), (1400, 768, 256)), ((1400, 512, 256), (1024, 2
 
 @pytest.mark.parametrize("cipher,lanes,layout,flags", [
     (CHACHA, 4, "fast", 0), (CHACHA, 8, "fast", 0), (CHACHA, 4, "packed", 0), (AES, 0, "fast", 0),
+    (CHACHA, 1, "fast", 0), (CHACHA, 1, "slot128", 0), (CHACHA, 0, "slot128", 0),
     (CHACHA, 4, "slot128", 0), (CHACHA, 8, "slot128", 0), (AES, 0, "slot128", 0),
     (AES, 0, "slot128", FLAG_CT_GHASH), (CHACHA, 4, "slot128", FLAG_VERIFY_FIRST),
     (AES, 0, "slot128", FLAG_VERIFY_FIRST)])

@@ -13,8 +13,10 @@ run() {  # name counters...
       python3 $R/bench.py --config $CFG --no-cpu-baseline --no-verify --settle-ms 0 --steps 10 --warmup 2 $EXTRA > $OUT/$name.log 2>&1
   echo "pmc $name rc=$?"
 }
-run fetch FETCH_SIZE || exit 1
-run write WRITE_SIZE || exit 1
-run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS GRBM_GUI_ACTIVE || exit 1
-run busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY || exit 1
-run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum || exit 1
+# PMC_GROUPS: a subset of the passes (default all five)
+G=" ${PMC_GROUPS:-fetch write sq busy tcc} "
+case "$G" in *" fetch "*) run fetch FETCH_SIZE || exit 1;; esac
+case "$G" in *" write "*) run write WRITE_SIZE || exit 1;; esac
+case "$G" in *" sq "*) run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS GRBM_GUI_ACTIVE || exit 1;; esac
+case "$G" in *" busy "*) run busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY || exit 1;; esac
+case "$G" in *" tcc "*) run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum || exit 1;; esac
