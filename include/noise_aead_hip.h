@@ -399,6 +399,9 @@ int noise_aead_debug_worker_placement(void);
  *   the host, ns from its start: packed, doorbell, done seen, returned. */
 void noise_aead_debug_worker_host_ns(uint64_t *out, int n);
 void *noise_aead_debug_last_freed_ctx(size_t *bytes);
+/* noise_aead_debug_workers_resident: resident single-call workers of the
+ *   current device whose kernel is still running (-1: no device). */
+int noise_aead_debug_workers_resident(void);
 
 /* Default lanes per record the library picks for a uniform batch of n
  * records in a FAST layout (16-B aligned slots readable up to roundup64(len)):

@@ -112,6 +112,44 @@ NA_DEV void chacha20_block_pre(const uint32_t key[8], const ChaPre &p, uint32_t 
     x[12] += ctr; x[14] += iv_lo; x[15] += iv_hi;
 }
 
+/* Two blocks of one key and nonce (counters c0, c1) in lock step: eight
+   independent quarter-round chains per half round instead of four, for a
+   wave that runs alone on its SIMD (the one-lane kernels' last wave). */
+NA_DEV void chacha20_2block_pre(const uint32_t key[8], const ChaPre &p, uint32_t c0, uint32_t c1,
+                                uint32_t iv_lo, uint32_t iv_hi, uint32_t x[16], uint32_t y[16])
+{
+#define NA_COL0(z, ctr)                                                   \
+    {                                                                     \
+        uint32_t a = p.a0, b = key[0], c = key[4], d = (ctr);             \
+        d ^= a; d = rotl(d, 16);                                          \
+        c += d; b ^= c; b = rotl(b, 12);                                  \
+        a += b; d ^= a; d = rotl(d, 8);                                   \
+        c += d; b ^= c; b = rotl(b, 7);                                   \
+        z[0] = a; z[4] = b; z[8] = c; z[12] = d;                          \
+        z[1] = p.c1[0]; z[5] = p.c1[1]; z[9] = p.c1[2]; z[13] = p.c1[3];  \
+        z[2] = p.c2[0]; z[6] = p.c2[1]; z[10] = p.c2[2]; z[14] = p.c2[3]; \
+        z[3] = p.c3[0]; z[7] = p.c3[1]; z[11] = p.c3[2]; z[15] = p.c3[3]; \
+    }
+    NA_COL0(x, c0)
+    NA_COL0(y, c1)
+#undef NA_COL0
+#define NA_QR2(i, j, k, l) NA_QR(x[i], x[j], x[k], x[l]); NA_QR(y[i], y[j], y[k], y[l])
+    NA_QR2(0, 5, 10, 15); NA_QR2(1, 6, 11, 12); NA_QR2(2, 7, 8, 13); NA_QR2(3, 4, 9, 14);
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        NA_QR2(0, 4, 8, 12); NA_QR2(1, 5, 9, 13); NA_QR2(2, 6, 10, 14); NA_QR2(3, 7, 11, 15);
+        NA_QR2(0, 5, 10, 15); NA_QR2(1, 6, 11, 12); NA_QR2(2, 7, 8, 13); NA_QR2(3, 4, 9, 14);
+    }
+#undef NA_QR2
+    const uint32_t k0[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { x[i] += k0[i]; y[i] += k0[i]; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { x[4 + i] += key[i]; y[4 + i] += key[i]; }
+    x[12] += c0; x[14] += iv_lo; x[15] += iv_hi;
+    y[12] += c1; y[14] += iv_lo; y[15] += iv_hi;
+}
+
 /* ------------------------------------------------------------- Poly1305 */
 
 constexpr uint32_t M26 = 0x3ffffffu;

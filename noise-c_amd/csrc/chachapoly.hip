@@ -1281,12 +1281,28 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
         if (m >= 1) solo_store(a, q.rec0, q.lane, m - 1, q.full_lim, nxt, 0xffu);
         __builtin_amdgcn_wave_barrier();
         if (m + 1 < q.S) solo_dma(a, q.rec0, q.lane, m + 1, q.lim, nxt);
+        /* Two waves share a SIMD and the older one takes the issue slots:
+           without this the pair ran nearly one after the other and the
+           second finished alone, at one wave's issue rate.  A wave that is
+           ahead lowers its priority (aead_device.h): C2 +5-8 %, C4 +0.5 %
+           (profiles/r04/solo_prio_ab.jsonl). */
+        prio_by_progress(m, q.S);
+#ifdef NA_SOLO_X2
+        uint32_t xs[2][16];
+        if (2 * m + 1 < q.J) chacha20_2block_pre(key, pre, 2 * m + 1, 2 * m + 2, n_lo, n_hi, xs[0], xs[1]);
+        else chacha20_block_pre(key, pre, 2 * m + 1, n_lo, n_hi, xs[0]);
+#endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u; /* unit, ChaCha block j + 1 */
             if (j < q.J) {
                 uint32_t x[16], w[16];
+#ifdef NA_SOLO_X2
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
+#else
                 chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+#endif
                 uint32_t nb = 4;
                 if constexpr (OPEN) {
 #pragma unroll

@@ -15,6 +15,10 @@ namespace na {
 
 inline int hip_rc(hipError_t e) { return e == hipSuccess ? NOISE_ERROR_NONE : NOISE_ERROR_SYSTEM; }
 
+/* ---- worker.hip: before a batch launch of this many workgroups (asks the
+   device's resident single-call workers to leave when it fills every CU) */
+NA_HIDDEN void worker_park_for_batch(uint32_t workgroups);
+
 /* ---- launch_chacha.hip.  k = lanes per record; every call returns a
    NOISE_ERROR_* code (NOISE_ERROR_INVALID_PARAM for an unsupported k). */
 /* uniform batch; fast = FAST layout, ukey = every wave's records share one

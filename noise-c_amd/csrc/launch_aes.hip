@@ -110,12 +110,14 @@ int aes_uniform(const UniformArgs &a, bool open, bool ct, bool staged, hipStream
     if (a.n_records == 0) return NOISE_ERROR_NONE;
     if (staged) { /* one state per 256-record workgroup + FAST layout */
         const uint32_t blocks = (a.n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
+        worker_park_for_batch(blocks);
         hipLaunchKernelGGL(ct ? (open ? gcm_staged<true, true> : gcm_staged<false, true>)
                               : (open ? gcm_staged<true, false> : gcm_staged<false, false>),
                            dim3(blocks), dim3(GCM_WG), 0, s, a);
         return hip_rc(hipGetLastError());
     }
     const uint32_t blocks = (uint32_t)(((uint64_t)a.n_records * GCM_LANES + 255) / 256);
+    worker_park_for_batch(blocks);
     hipLaunchKernelGGL(ct ? (open ? gcm_uniform<true, true> : gcm_uniform<false, true>)
                           : (open ? gcm_uniform<true, false> : gcm_uniform<false, false>),
                        dim3(blocks), dim3(256), 0, s, a);
@@ -139,6 +141,7 @@ int aes_duplex(const UniformArgs &a, const UniformArgs &b, bool ct, hipStream_t 
 {
     const uint32_t sb = (a.n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
     const uint32_t ob = (b.n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
+    worker_park_for_batch(sb > ob ? sb : ob);
     if (gcm_duplex_fused_on()) {
         hipLaunchKernelGGL(ct ? gcm_duplex_fused<true> : gcm_duplex_fused<false>,
                            dim3(sb > ob ? sb : ob), dim3(GCM_WG), 0, s, a, b, sb, ob);
@@ -165,6 +168,7 @@ int aes_ragged(const RaggedArgs &a, bool open, bool fast, bool ct, bool wide, hi
     const uint32_t per = (uint32_t)(sh.wg / sh.kl * sh.r); /* records per window */
     const uint32_t blocks = (a.n_records + per - 1) / per;
     KernelFn<RaggedArgs> fn = ct ? gcm_ragged_fn<true>(open, fast, sh) : gcm_ragged_fn<false>(open, fast, sh);
+    worker_park_for_batch(blocks);
     hipLaunchKernelGGL(fn, dim3(blocks), dim3(sh.wg), 0, s, a);
     return hip_rc(hipGetLastError());
 }

@@ -23,6 +23,7 @@ int launch(KernelFn<Args> fn, uint32_t n_records, int lanes, const Args &a, hipS
     if (n_records == 0) return NOISE_ERROR_NONE;
     const uint64_t threads = (uint64_t)n_records * lanes;
     const uint32_t blocks = (uint32_t)((threads + 255) / 256);
+    worker_park_for_batch(blocks);
     hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, s, a);
     return hip_rc(hipGetLastError());
 }
@@ -146,6 +147,7 @@ int duplex_persist_launch(const UniformArgs &a, const UniformArgs &b, hipStream_
     const uint32_t sj = (uint32_t)(((uint64_t)a.n_records * K + 63) / 64);
     const uint32_t oj = (uint32_t)(((uint64_t)b.n_records * K + 63) / 64);
     const uint32_t want = (sj + oj + 3) / 4;
+    worker_park_for_batch(want);
     hipLaunchKernelGGL(fn, dim3(want < resident ? want : resident), dim3(256), 0, s, a, b, sj, oj, ctr);
     return hip_rc(hipGetLastError());
 }
@@ -173,6 +175,7 @@ int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, 
     else if (k == 4) fn = ukey ? chachapoly_duplex_staged<4, true> : chachapoly_duplex_staged<4, false>;
     else if (k == 8) fn = ukey ? chachapoly_duplex_staged<8, true> : chachapoly_duplex_staged<8, false>;
     else return NOISE_ERROR_INVALID_PARAM;
+    worker_park_for_batch(sb + ob);
     hipLaunchKernelGGL(fn, dim3(sb + ob), dim3(256), 0, s, a, b, sb, ob);
     return hip_rc(hipGetLastError());
 }

@@ -28,8 +28,12 @@
  * thread of the workgroup (one barrier-synchronised loop).  Before leaving it
  * sets `exiting` and looks at seq once more, so a request posted meanwhile
  * is either served or seen by the host (exiting set, done behind): the host
- * then waits for the stream and starts a new worker at the same seq.  At most
- * one worker per device is alive; calls on it are serialised by a mutex.
+ * then waits for the stream and starts a new worker at the same seq.  A
+ * device runs up to kWorkersPerDev workers, each with its own slot and
+ * stream: a calling thread takes a free one without waiting (its own first),
+ * so N threads on N CipherStates make N calls at once, as on the CPU.  Batch
+ * launches that fill every CU ask the resident workers to leave first
+ * (worker_park_for_batch), so no batch workgroup waits for a worker's CU.
  *
  * Key material reaches the worker through the slot as well: the ChaCha key
  * itself, or for AES-GCM a pinned host copy of the state's device context
@@ -51,6 +55,7 @@
 #include <emmintrin.h>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <ctime>
 
@@ -591,6 +596,7 @@ namespace {
 struct Worker {
     std::mutex mu;
     int state = 0;             /* 0 unknown, 1 usable, -1 disabled */
+    int launch_fails = 0;      /* consecutive failed launches (3 disable the worker) */
     WorkerSlot *slot = nullptr; /* host view */
     WorkerSlot *dslot = nullptr; /* device view */
     /* the request (header chunks, stream): in fine-grained device memory the
@@ -604,30 +610,67 @@ struct Worker {
     uint8_t *out = nullptr, *dout = nullptr;   /* raw results */
     hipStream_t stream = nullptr;
     uint32_t seq = 0;
-    bool launched = false;
+    bool launched = false;     /* written under mu, read by park() with atomics */
 };
 
 constexpr int kMaxDev = 64;
-Worker g_worker[kMaxDev];
+/* Resident workers a device may run at once.  A CipherState is single-owner
+   with no locks (cipherstate.c:293-410), so N threads calling on N states
+   run N calls at once on the CPU; here each calling thread gets a worker of
+   its own (a workgroup on its own CU, launched on first use and gone 2 ms
+   after its last request), claimed without waiting while one is free. */
+constexpr int kWorkersPerDev = 8;
+Worker g_worker[kMaxDev][kWorkersPerDev];
+std::atomic<uint32_t> g_next_pref{0};
+thread_local int t_pref = -1;             /* this thread's first-choice worker */
+thread_local Worker *t_last = nullptr;    /* the worker of this thread's last call (debug hooks) */
 std::once_flag g_atexit_once;
 
 constexpr uint64_t IDLE_TICKS = 200000;       /* 2 ms at 100 MHz */
+/* Test hook: NOISE_AEAD_DEBUG_WORKER_IDLE_MS overrides the idle timeout. */
+uint64_t idle_ticks()
+{
+    static const uint64_t v = [] {
+        const char *e = getenv("NOISE_AEAD_DEBUG_WORKER_IDLE_MS");
+        return e && atoi(e) > 0 ? (uint64_t)atoi(e) * 100000ull : IDLE_TICKS;
+    }();
+    return v;
+}
 constexpr uint64_t LIFETIME_TICKS = 500000000; /* 5 s */
+/* The longest request (a 65519-B AES-GCM record) takes ~0.4 ms; a worker
+   that has not answered after this is taken for lost: the call falls back to
+   the launch path and the worker is not used again. */
+constexpr uint64_t WAIT_LIMIT_NS = 2000000000ull; /* 2 s */
 
 /* the header's stop field: chunk 2 word 3 (host memory), chunk 5 word 1 (device) */
 uint32_t *stop_word(Worker &w) { return w.vram ? &w.req[4 * 5 + 1] : &w.req[4 * 2 + 3]; }
 
+/* Ask every launched worker of device dev to leave (no wait).  A worker
+   leaving scrubs its LDS; a request racing with the stop is either served or
+   seen by its caller as `exiting` (the caller then starts a new worker). */
+void park_device(int dev)
+{
+    for (int i = 0; i < kWorkersPerDev; ++i) {
+        Worker &w = g_worker[dev][i];
+        if (__atomic_load_n(&w.launched, __ATOMIC_ACQUIRE)) {
+            __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
+            _mm_sfence();
+        }
+    }
+}
+
 void worker_stop_all()
 {
-    for (int d = 0; d < kMaxDev; ++d) {
-        Worker &w = g_worker[d];
-        std::lock_guard<std::mutex> lk(w.mu);
-        if (w.state != 1 || !w.launched) continue;
-        __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
-        _mm_sfence();
-        (void)hipStreamSynchronize(w.stream);
-        w.launched = false;
-    }
+    for (int d = 0; d < kMaxDev; ++d)
+        for (int i = 0; i < kWorkersPerDev; ++i) {
+            Worker &w = g_worker[d][i];
+            std::lock_guard<std::mutex> lk(w.mu);
+            if (w.state != 1 || !w.launched) continue;
+            __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
+            _mm_sfence();
+            (void)hipStreamSynchronize(w.stream);
+            __atomic_store_n(&w.launched, false, __ATOMIC_RELEASE);
+        }
 }
 
 bool worker_enabled()
@@ -688,23 +731,108 @@ int worker_setup(Worker &w, int dev)
     return 1;
 }
 
+/* NOISE_ERROR_NONE, or NOISE_ERROR_NOT_APPLICABLE (the caller takes the
+   launch path; three failures in a row retire the worker) */
+/* Test hook: NOISE_AEAD_DEBUG_WORKER_FAIL=1 makes every worker launch fail
+   (tests/test_gpu_worker.py: the calls must then take the launch path). */
+bool debug_launch_fails()
+{
+    static const bool v = [] {
+        const char *e = getenv("NOISE_AEAD_DEBUG_WORKER_FAIL");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+/* NOISE_AEAD_WORKER_PARK=0: batch launches leave the workers resident (the
+   A/B of tests/test_gpu_worker.py's batch-beside-worker measurement). */
+bool park_enabled()
+{
+    static const bool v = [] {
+        const char *e = getenv("NOISE_AEAD_WORKER_PARK");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 int worker_launch(Worker &w)
 {
     (void)hipStreamSynchronize(w.stream); /* a previous worker has left */
+    if (debug_launch_fails()) {
+        if (++w.launch_fails >= 3) w.state = -1;
+        return NOISE_ERROR_NOT_APPLICABLE;
+    }
     __atomic_store_n(&w.slot->exiting, 0u, __ATOMIC_RELEASE);
     __atomic_store_n(stop_word(w), 0u, __ATOMIC_RELEASE);
     _mm_sfence();
     hipLaunchKernelGGL(aead_worker, dim3(1), dim3(256), 0, w.stream, w.dslot, w.dreq, (const uint4 *)w.din,
-                       w.vram ? 1u : 0u, (const uint8_t *)w.dtail, w.dout, w.seq, IDLE_TICKS, LIFETIME_TICKS);
-    if (hipGetLastError() != hipSuccess) return NOISE_ERROR_SYSTEM;
-    w.launched = true;
+                       w.vram ? 1u : 0u, (const uint8_t *)w.dtail, w.dout, w.seq, idle_ticks(), LIFETIME_TICKS);
+    if (hipGetLastError() != hipSuccess) {
+        if (++w.launch_fails >= 3) w.state = -1;
+        return NOISE_ERROR_NOT_APPLICABLE;
+    }
+    w.launch_fails = 0;
+    __atomic_store_n(&w.launched, true, __ATOMIC_RELEASE);
     return NOISE_ERROR_NONE;
 }
+
+/* A usable worker of device dev, locked: this thread's own if free, else
+   the first free one, else wait for this thread's own.  nullptr: none usable
+   (set up failed on all of them). */
+Worker *claim_worker(int dev, std::unique_lock<std::mutex> &lk)
+{
+    if (t_pref < 0) t_pref = (int)(g_next_pref.fetch_add(1, std::memory_order_relaxed) % kWorkersPerDev);
+    for (int i = 0; i < kWorkersPerDev; ++i) {
+        Worker &w = g_worker[dev][(t_pref + i) % kWorkersPerDev];
+        std::unique_lock<std::mutex> l(w.mu, std::try_to_lock);
+        if (!l.owns_lock()) continue;
+        if (worker_setup(w, dev) != 1) continue;
+        lk = std::move(l);
+        return &w;
+    }
+    for (int i = 0; i < kWorkersPerDev; ++i) {
+        Worker &w = g_worker[dev][(t_pref + i) % kWorkersPerDev];
+        std::unique_lock<std::mutex> l(w.mu);
+        if (worker_setup(w, dev) != 1) continue;
+        lk = std::move(l);
+        return &w;
+    }
+    return nullptr;
+}
+
+int g_cus[kMaxDev]; /* compute units per device (0: not read yet) */
 
 } // namespace
 
 
 extern "C" NA_HIDDEN int na_worker_enabled(void) { return worker_enabled() ? 1 : 0; }
+
+/* A batch launch of `workgroups` workgroups on the current device: when it
+   fills every CU, the resident workers of the device are asked to leave
+   first.  A worker holds ~151 KB of its CU's LDS, so a batch workgroup
+   placed on that CU could not start until it left (2 ms after its last
+   request): the batch kernels are single generations per CU (C2: two
+   one-lane workgroups per CU, C3: one AES-GCM workgroup), and one CU short
+   would run a second generation on another CU. */
+NA_HIDDEN void worker_park_for_batch(uint32_t workgroups)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
+    int cus = __atomic_load_n(&g_cus[dev], __ATOMIC_RELAXED);
+    if (!cus) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return;
+        __atomic_store_n(&g_cus[dev], cus, __ATOMIC_RELAXED);
+    }
+    if (workgroups >= (uint32_t)cus && park_enabled()) park_device(dev);
+}
+
+/* A state's AES-GCM context is being freed: every worker that may hold it in
+   its LDS cache leaves (and scrubs its LDS on the way out). */
+extern "C" NA_HIDDEN void na_worker_forget_ctx(void)
+{
+    for (int d = 0; d < kMaxDev; ++d) park_device(d);
+}
 
 namespace {
 
@@ -753,9 +881,11 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
         return NOISE_ERROR_NOT_APPLICABLE;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return NOISE_ERROR_NOT_APPLICABLE;
-    Worker &w = g_worker[dev];
-    std::lock_guard<std::mutex> lk(w.mu);
-    if (worker_setup(w, dev) != 1) return NOISE_ERROR_NOT_APPLICABLE;
+    std::unique_lock<std::mutex> lk;
+    Worker *wp = claim_worker(dev, lk);
+    if (!wp) return NOISE_ERROR_NOT_APPLICABLE;
+    Worker &w = *wp;
+    t_last = wp;
     void *d_hctx = nullptr;
     if (h_ctx && hipHostGetDevicePointer(&d_hctx, (void *)h_ctx, 0) != hipSuccess)
         return NOISE_ERROR_NOT_APPLICABLE;
@@ -763,7 +893,7 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     WorkerSlot *s = w.slot;
     if (!w.launched || __atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE)) {
         const int rc = worker_launch(w);
-        if (rc) return rc;
+        if (rc) return rc; /* nothing posted yet */
     }
     const uint32_t k = ++w.seq;
     /* the input stream key || AD || pad || record (|| tag): its first head
@@ -816,45 +946,63 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     }
     _mm_sfence(); /* out of the write-combining buffer now, not later */
     const uint64_t h2 = host_ns();
+    /* From here on every exit scrubs the shared memory below.  A failure the
+       worker caused (a relaunch that fails, a stale input, no answer within
+       WAIT_LIMIT_NS) is NOISE_ERROR_NOT_APPLICABLE: the caller runs the
+       record through the launch path with the same nonce instead — the result
+       is the same bytes, and the worker only ever writes w.out and the slot. */
+    int st = NOISE_ERROR_NONE;
     uint64_t spins = 0;
     while (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
         __builtin_ia32_pause();
-        if ((++spins & 1023) == 0 && __atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE) &&
-            __atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
+        if ((++spins & 1023) != 0) continue;
+        if (__atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE) && __atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
             /* the worker left before it took k: start one at k - 1 */
-            if (hipStreamSynchronize(w.stream) != hipSuccess) return NOISE_ERROR_SYSTEM;
+            if (hipStreamSynchronize(w.stream) != hipSuccess) {
+                w.state = -1;
+                st = NOISE_ERROR_NOT_APPLICABLE;
+                break;
+            }
             if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == k) break;
             w.seq = k - 1;
             const int rc = worker_launch(w);
             w.seq = k;
-            if (rc) return rc;
+            if (rc) {
+                st = rc;
+                break;
+            }
         }
-        if (spins > (1ull << 32)) return NOISE_ERROR_SYSTEM; /* never in practice */
+        if (host_ns() - h2 > WAIT_LIMIT_NS) { /* lost: never used again */
+            w.state = -1;
+            st = NOISE_ERROR_NOT_APPLICABLE;
+            break;
+        }
     }
     const uint64_t h3 = host_ns();
-    const uint32_t status = s->status;
-    const int st = status == 2 ? NOISE_ERROR_SYSTEM : (status ? NOISE_ERROR_MAC_FAILURE : NOISE_ERROR_NONE);
-    if (st == NOISE_ERROR_NONE) memcpy(data, w.out, open ? len : len + 16);
+    if (st == NOISE_ERROR_NONE) {
+        const uint32_t status = s->status;
+        st = status == 2 ? NOISE_ERROR_NOT_APPLICABLE : (status ? NOISE_ERROR_MAC_FAILURE : NOISE_ERROR_NONE);
+        if (st == NOISE_ERROR_NONE) memcpy(data, w.out, open ? len : len + 16);
+    }
     /* key, plaintext and results out of the shared host memory; the stamps
-       stay (a zeroed chunk would carry number 0, which no request has) */
+       stay (a zeroed chunk would carry number 0, which no request has).  The
+       worker writes its results in 16-B pieces: up to roundup16(len + 16). */
     for (size_t c = 0; c < nchunks; ++c) _mm_store_si128((__m128i *)(w.in + c), w.vram ? vstamp : stamp);
     if (total > head) explicit_bzero(w.tail, total - head);
     if (w.vram) _mm_sfence();
-    explicit_bzero(w.out, len + 16);
+    explicit_bzero(w.out, (len + 16 + 15) & ~(size_t)15);
     const uint64_t h4 = host_ns();
     t_host[0] = h1 - h0; t_host[1] = h2 - h0; t_host[2] = h3 - h0; t_host[3] = h4 - h0;
     return st;
 }
 
-/* Test hook: the phase stamps of this device's last worker request, in
+/* Test hook: the phase stamps of this thread's last worker request, in
    10-ns ticks relative to the moment the worker saw it: [0] fence done, [1]
    record and context in LDS, [2] computed, [3] results written, [4] release
    done; n = 5. */
 extern "C" void noise_aead_debug_worker_stamps(uint32_t *out, int n)
 {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
-    const WorkerSlot *s = g_worker[dev].slot;
+    const WorkerSlot *s = t_last ? t_last->slot : nullptr;
     for (int i = 0; i < n && i < 5; ++i) out[i] = s ? s->stamps[i + 1] - s->stamps[0] : 0;
 }
 
@@ -869,29 +1017,35 @@ extern "C" void noise_aead_debug_worker_host_ns(uint64_t *out, int n)
    start: ChaCha, CT in LDS, Poly blocks loaded, tree, tag, open's write). */
 extern "C" void noise_aead_debug_worker_fast_stamps(uint32_t *out, int n)
 {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
-    const WorkerSlot *s = g_worker[dev].slot;
+    const WorkerSlot *s = t_last ? t_last->slot : nullptr;
     for (int i = 0; i < n && i < 8; ++i) out[i] = s ? s->fstamps[i] : 0;
 }
 
-/* Test hook: 0 no worker set up on this device, 1 requests in pinned host
-   memory, 2 in device memory. */
+/* Test hook: the placement of this thread's last worker: 0 none set up, 1
+   requests in pinned host memory, 2 in device memory. */
 extern "C" int noise_aead_debug_worker_placement(void)
 {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
-    const Worker &w = g_worker[dev];
-    return w.state != 1 ? 0 : (w.vram ? 2 : 1);
+    const Worker *w = t_last;
+    return !w || w->state != 1 ? 0 : (w->vram ? 2 : 1);
 }
 
 /* Test hook: the shader clock (MHz) of the last worker request's compute
    phase (s_memtime cycles over s_memrealtime time). */
+extern "C" int noise_aead_debug_workers_resident(void)
+{
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return -1;
+    for (int i = 0; i < kWorkersPerDev; ++i) {
+        Worker &w = g_worker[dev][i];
+        std::lock_guard<std::mutex> lk(w.mu);
+        if (w.state == 1 && w.launched && hipStreamQuery(w.stream) == hipErrorNotReady) ++n;
+    }
+    return n;
+}
+
 extern "C" double noise_aead_debug_worker_clock_mhz(void)
 {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0.0;
-    const WorkerSlot *s = g_worker[dev].slot;
+    const WorkerSlot *s = t_last ? t_last->slot : nullptr;
     if (!s || s->stamps[3] == s->stamps[2]) return 0.0;
     return (double)s->stamps[6] / ((double)(s->stamps[3] - s->stamps[2]) * 0.01);
 }

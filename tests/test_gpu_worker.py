@@ -102,3 +102,75 @@ def test_worker_in_place_buffer_semantics(aead, gpu, oracle):
     assert bytes(mem)[:L + 16] == oracle.encrypt(CHACHA, key, 0, pt)
     assert bytes(mem)[L + 16:] == bytes([0xAB]) * 48
     st.free()
+
+
+def _child(script, env_extra, timeout=110):
+    env = dict(os.environ, **env_extra)
+    r = subprocess.run([sys.executable, "-u", os.path.join(os.path.dirname(__file__), script)],
+                       env=env, timeout=timeout, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    return r.stdout
+
+
+def test_batch_beside_resident_worker(gpu):
+    """A C2-sized batch launched right after a single call (the worker still
+    resident on its CU) takes the time of the same batch on a device with no
+    worker: batch launches that fill every CU ask the workers to leave first
+    (worker_park_for_batch).  The unparked cost is measured beside it
+    (NOISE_AEAD_WORKER_PARK=0) and reported, not asserted."""
+    import json
+    parked = json.loads(_child("worker_batch_check.py", {}).strip().splitlines()[-1])
+    unparked = json.loads(_child("worker_batch_check.py", {"NOISE_AEAD_WORKER_PARK": "0"})
+                          .strip().splitlines()[-1])
+    print("parked", parked["ratio"], "unparked", unparked["ratio"])
+    assert max(parked["resident_before_warm"]) >= 1  # the single call did leave a worker
+    assert parked["ratio"] <= 1.05, parked
+
+
+def _tool(name):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "tools", name)
+    if not os.path.exists(path):
+        pytest.skip(f"tools/{name} not built (tools/build_latency.sh)")
+    return path
+
+
+def test_single_calls_scale_over_threads(gpu):
+    """T threads on T CipherStates make T single calls at once (each thread
+    takes a resident worker of its own, as T CPU threads would each run the
+    reference's cipherstate.c:293-410 without a lock): 8 threads reach at
+    least 4x the call rate of one (tools/mt_calls: 1400-B encrypt + decrypt
+    per iteration, every record checked)."""
+    import json
+    tool = _tool("mt_calls")
+    rates = {}
+    for t in (1, 8):
+        r = subprocess.run([tool, "chachapoly", str(t), "1400", "1.0"], timeout=60,
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["ok"]
+        rates[t] = d["calls_per_s"]
+    print("calls/s", rates)
+    assert rates[8] >= 4 * rates[1], rates
+
+
+def test_worker_launch_failure_falls_back(gpu):
+    """A worker that cannot be launched (NOISE_AEAD_DEBUG_WORKER_FAIL=1) costs
+    no call: every record takes the launch path with the same nonce and
+    result (vs the oracle), nonces advance once per call, and the failed
+    workers are retired."""
+    out = _child("worker_mode_check.py", {"NOISE_AEAD_DEBUG_WORKER_FAIL": "1"})
+    assert int(out.split("placement")[-1].split()[0]) == 0, out
+
+
+def test_freed_aes_state_clears_worker_cache(gpu):
+    """An AES-GCM state's context is cached in a worker's LDS by its single
+    calls; freeing the state makes every worker that may hold it leave, and
+    a leaving worker zeroes its LDS cache (worker.hip, after its loop).  The
+    child runs with a 10 s idle timeout, so only the free can end it."""
+    env = {"NOISE_AEAD_DEBUG_WORKER_IDLE_MS": "10000"}
+    r = subprocess.run([sys.executable, "-u", os.path.join(os.path.dirname(__file__), "worker_mode_check.py"),
+                        "--free-check"], env=dict(os.environ, **env), timeout=110, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert float(r.stdout.split("left_ms")[-1].split()[0]) >= 0

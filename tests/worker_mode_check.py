@@ -55,5 +55,30 @@ def main():
     return 0
 
 
+def free_check():
+    """--free-check (run with NOISE_AEAD_DEBUG_WORKER_IDLE_MS=10000, so no
+    worker leaves by idling): an AES-GCM single call leaves the worker
+    resident with the state's context cached in LDS; freeing the state must
+    make it leave (it zeroes that cache on the way out) within 200 ms.
+    Prints "left_ms X"."""
+    import time
+    lib = aead.lib()
+    lib.noise_aead_debug_workers_resident.restype = int
+    _, st = aead.CipherState.new_by_id(0x4302)
+    assert st.init_key(bytes(range(32))) == 0
+    st.seal(bytes(100))
+    time.sleep(0.05)
+    if lib.noise_aead_debug_workers_resident() < 1:
+        print("no resident worker after the call")
+        return 1
+    t0 = time.time()
+    st.free()
+    while lib.noise_aead_debug_workers_resident() and time.time() - t0 < 0.2:
+        time.sleep(0.001)
+    left = lib.noise_aead_debug_workers_resident() == 0
+    print("left_ms", round((time.time() - t0) * 1e3, 3) if left else -1)
+    return 0 if left else 1
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(free_check() if "--free-check" in sys.argv else main())

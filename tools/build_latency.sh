@@ -1,6 +1,9 @@
 #!/bin/sh
-# Builds tools/latency (single-record GPU CipherState latency, tools/latency.c).
+# Builds tools/latency (single-record GPU CipherState latency, tools/latency.c)
+# and tools/mt_calls (single-call throughput over threads, tools/mt_calls.c).
 set -e
 cd "$(dirname "$0")/.."
 gcc -O2 -Iinclude tools/latency.c -Lnoise-c_amd/lib -lnoise_aead_hip \
     -Wl,-rpath,'$ORIGIN/../noise-c_amd/lib' -o tools/latency
+gcc -O2 -pthread -Iinclude tools/mt_calls.c -Lnoise-c_amd/lib -lnoise_aead_hip \
+    -Wl,-rpath,'$ORIGIN/../noise-c_amd/lib' -o tools/mt_calls
