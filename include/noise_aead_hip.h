@@ -198,8 +198,12 @@ int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_
  *       cipher-aesgcm.c:172-188): a rejected record's output is not written
  *       at all, not even zeroed.
  * Memory: input and output records must be either exactly in place
- * (in == out and in_stride == out_stride) or fully disjoint; any partial
- * overlap is refused with NOISE_ERROR_INVALID_PARAM.
+ * (in == out and in_stride == out_stride) or disjoint record by record:
+ * with one stride for both sides the records may interleave (input and
+ * output slots alternating in one buffer) as long as no input record
+ * [in + i*stride, + len (+16 open)) meets an output record; with two
+ * strides the two spans must be disjoint.  Anything else is refused with
+ * NOISE_ERROR_INVALID_PARAM.
  * lanes_per_record: 0 = automatic; ChaChaPoly 1, 2, 4, 8, 16, 32 or 64 (wider
  * groups cut the latency of small batches of long records); AESGCM 4 (0 lets
  * a ragged batch of at most 512 records run one record per workgroup). */

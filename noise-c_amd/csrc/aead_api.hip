@@ -90,6 +90,23 @@ void job_span(const NoiseAeadUniform *j, bool out, bool open, uint64_t &lo, uint
    be exactly in place (in == out, one stride): records whose input and output
    spans overlap any other way would race with their neighbours' reads (and a
    rejected record's scrub would wipe input other records still need). */
+int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); } /* b > 0 */
+
+/* Does any input record [in + i s, in + i s + rin) meet any output record
+   [out + k s, out + k s + rout), i, k < n, one stride s for both?  With
+   d = out - in they meet iff some m = i - k, |m| < n, has
+   d - rin < m s < d + rout. */
+bool strided_records_meet(uint64_t in, uint64_t out, uint64_t s, uint64_t rin, uint64_t rout, uint32_t n)
+{
+    if (!rin || !rout || !n) return false;
+    const int64_t d = (int64_t)(out - in), st = (int64_t)s;
+    const int64_t m_lo = floor_div(d - (int64_t)rin, st) + 1;  /* smallest m with m s > d - rin */
+    const int64_t m_hi = -floor_div(-(d + (int64_t)rout), st) - 1; /* largest m with m s < d + rout */
+    const int64_t lo = m_lo > -(int64_t)(n - 1) ? m_lo : -(int64_t)(n - 1);
+    const int64_t hi = m_hi < (int64_t)(n - 1) ? m_hi : (int64_t)(n - 1);
+    return lo <= hi;
+}
+
 int check_uniform(const NoiseAeadUniform *j, bool open)
 {
     if (!j || !j->ctx || !j->nonce_base || !j->in || !j->out || !j->recs_per_state)
@@ -98,10 +115,20 @@ int check_uniform(const NoiseAeadUniform *j, bool open)
     if (j->len > NOISE_MAX_PAYLOAD_LEN - 16) return NOISE_ERROR_INVALID_LENGTH;
     if ((uintptr_t)j->ctx & 15) return NOISE_ERROR_INVALID_PARAM;
     if (j->n_records && !(j->in == j->out && j->in_stride == j->out_stride)) {
-        uint64_t il, ih, ol, oh;
-        job_span(j, false, open, il, ih);
-        job_span(j, true, open, ol, oh);
-        if (il < oh && ol < ih) return NOISE_ERROR_INVALID_PARAM;
+        /* records of one stride may interleave (input and output slots
+           alternating in one buffer) as long as no two of them meet; other
+           layouts need disjoint spans */
+        const uint64_t rin = (uint64_t)j->len + (open ? 16u : 0u), rout = (uint64_t)j->len + (open ? 0u : 16u);
+        if (j->in_stride == j->out_stride && j->in_stride >= rin && j->in_stride >= rout) {
+            if (strided_records_meet((uint64_t)(uintptr_t)j->in, (uint64_t)(uintptr_t)j->out, j->in_stride,
+                                     rin, rout, j->n_records))
+                return NOISE_ERROR_INVALID_PARAM;
+        } else {
+            uint64_t il, ih, ol, oh;
+            job_span(j, false, open, il, ih);
+            job_span(j, true, open, ol, oh);
+            if (il < oh && ol < ih) return NOISE_ERROR_INVALID_PARAM;
+        }
     }
     return NOISE_ERROR_NONE;
 }

@@ -373,6 +373,9 @@ NA_DEV uint4 load_sys16_raw(const uint8_t *p)
     return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
 }
 
+/* polls without a request after which only the header is polled: 20 us */
+constexpr uint64_t POLL_BACKOFF = 2000;
+
 /* 256 threads.  req: the header chunks (4 in host memory; 8 in device
    memory, vram); in: the stream's stamped chunks, tail: the rest raw; last:
    the last request already served; idle/lifetime in s_memrealtime ticks
@@ -403,13 +406,21 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
     uint64_t quiet = born;
     bool leaving = false;
     uint32_t tick = 0;
+    __shared__ uint32_t s_slow; /* backed-off polling (see below) */
+    if (t == 0) s_slow = 0;
+    __syncthreads();
     for (;;) {
         uint32_t t_seen = 0;
         /* every thread reads input chunk t; wave 0's lanes 0..3 (0..7 in
            device memory) hold the header (other lanes read a header chunk
-           too: same round trip) */
-        uint4 c, mine;
-        load_sys16x2(req + 4 * (t & (vram ? 7 : 3)), (const uint32_t *)(in + t), c, mine);
+           too: same round trip).  After POLL_BACKOFF without a request only
+           wave 0 polls, the header alone (128 B instead of 8 KiB per poll:
+           with the request in host memory every poll crosses PCIe), and a
+           request then re-reads its chunks once (stamp 0 is never current).
+           A wave may see the previous poll's setting: both are correct. */
+        uint4 c = make_uint4(0, 0, 0, 0), mine = make_uint4(0, 0, 0, 0);
+        if (!s_slow) load_sys16x2(req + 4 * (t & (vram ? 7 : 3)), (const uint32_t *)(in + t), c, mine);
+        else if (t < 64) c = load_sys16(req + 4 * (t & (vram ? 7 : 3)));
         if (t == 0) s_stale = 0;
         if (t < 64) {
             const uint32_t s0 = __shfl((int)c.x, 0, 64);
@@ -448,9 +459,12 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
                        `exiting` set and the host starts a new worker */
                     NA_SYS_STORE(&slot->exiting, 1u);
                     leaving = true;
+                } else if (now - quiet > POLL_BACKOFF) {
+                    __builtin_amdgcn_s_sleep(8);
                 } else {
                     __builtin_amdgcn_s_sleep(2);
                 }
+                s_slow = cmd == 0 && now - quiet > POLL_BACKOFF ? 1u : 0u;
                 s_cmd = cmd;
                 t_seen = (uint32_t)now;
             }

@@ -225,6 +225,15 @@ def test_device_api_argument_rules(aead_built):
                 == A.ERROR_INVALID_PARAM
             assert A.dev_uniform(open_, cid, **{**ok, "out": fake + 4 * 1408 - 16}) \
                 == A.ERROR_INVALID_PARAM
+            # one stride, input and output slots alternating in one buffer
+            # (ADVICE r3): accepted while no two records meet, refused once
+            # an output record reaches into an input record
+            inter = {**ok, "in_stride": 2848, "out_stride": 2848}
+            assert A.dev_uniform(open_, cid, **{**inter, "out": fake + 1424}) != A.ERROR_INVALID_PARAM
+            assert A.dev_uniform(open_, cid, **{**inter, "out": fake - 1424}) != A.ERROR_INVALID_PARAM
+            assert A.dev_uniform(open_, cid, **{**inter, "out": fake + 1408}) \
+                == (A.ERROR_INVALID_PARAM if open_ else A.dev_uniform(open_, cid, **{**inter, "out": fake + 1424}))
+            assert A.dev_uniform(open_, cid, **{**inter, "out": fake + 1000}) == A.ERROR_INVALID_PARAM
 
 
 def test_duplex_independence_rules(aead_built):

@@ -836,3 +836,41 @@ def test_full_size_config(aead, gpu, oracle, cipher):
     back = d_back.cpu().numpy().reshape(N, in_stride)[:, :L]
     assert np.array_equal(back[mask], pt_h.reshape(N, in_stride)[:, :L][mask])
     assert np.all(back[~mask] == 0)
+
+
+@pytest.mark.parametrize("cipher", [CHACHA, AES])
+def test_interleaved_slots_one_buffer(aead, gpu, oracle, cipher):
+    """Input and output slots alternating in one buffer with one stride
+    (accepted since no two records meet): the seal writes every
+    output slot, leaves every input slot as it was, and matches the oracle;
+    the open back through the same interleaving restores the plaintext."""
+    torch = _torch()
+    rng = np.random.default_rng(2718 + (cipher & 3))
+    L, count, slot = 1400, 300, 1536
+    keys = rng.integers(0, 256, (1, 32), dtype=np.uint8)
+    nb = np.array([12345], dtype=np.uint64)
+    buf = rng.integers(0, 256, 2 * slot * count + 64, dtype=np.uint8)
+    pt = buf.copy()
+    exp = oracle_seal_records(oracle, cipher, keys, nb, count, pt, 2 * slot, L, count, 2 * slot)
+    ctx, _k = prepare(aead, cipher, keys)
+    d_nb = dev(nb.view(np.int64))
+    d = dev(buf)
+    base = d.data_ptr()
+    common = dict(ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(), in_stride=2 * slot,
+                  out_stride=2 * slot, length=L, n_records=count, recs_per_state=count, stream=stream())
+    assert aead.dev_uniform(False, cipher, inp=base, out=base + slot, **common) == 0
+    sync()
+    got = d.cpu().numpy()
+    for i in range(count):
+        o = 2 * slot * i
+        assert np.array_equal(got[o:o + slot], pt[o:o + slot]), i  # input slot untouched
+        assert np.array_equal(got[o + slot:o + slot + L + 16], exp[o:o + L + 16]), i
+    st = torch.full((count,), 9, dtype=torch.uint8, device="cuda")
+    # open: read the output slots back into the input slots
+    assert aead.dev_uniform(True, cipher, inp=base + slot, out=base, status=st.data_ptr(), **common) == 0
+    sync()
+    back = d.cpu().numpy()
+    assert int(st.max().item()) == 0
+    for i in range(count):
+        o = 2 * slot * i
+        assert np.array_equal(back[o:o + L], pt[o:o + L]), i
