@@ -23,6 +23,7 @@
  */
 #include "aead_device.h"
 #include "aead_kernels.h"
+#include "aes_bs.h"
 
 namespace na {
 
@@ -940,6 +941,245 @@ __global__ __launch_bounds__(GCM_WG) void gcm_duplex_fused(UniformArgs s, Unifor
     if (b < o_blocks) gcm_staged_rec<true, CT>(o, TE, L.h4[1], L.rk[1], b);
 }
 
+/* ---------------------- bitsliced (uniform FAST, one state per workgroup)
+ *
+ * Round 4 (decide AES-GCM's structure in the full kernel).  A
+ * lane pair owns one record.  The record's counter blocks ctr = 0 .. run in
+ * groups of 32 (ctr 32g .. 32g+31): the pair computes a group's key stream
+ * with the bitsliced AES of aes_bs.h (no tables, constant-time), XORs it
+ * into the record's data (lane L: bytes 8L..8L+7 of every block) and feeds
+ * GHASH from registers.  GHASH position p of the GCM input (AD empty:
+ * p = 1..M the CT blocks, p = M + 1 = n the length block) is ctr p + 1, so
+ * group g holds positions 32g - 1 .. 32g + 30; lane L runs Horner with H
+ * over the 16 positions 32g + 16L - 1 .. (one DPP exchange makes its blocks
+ * whole), jumping over the partner's 16 with H^16 = (H^8)^2 between groups.
+ * With e_L its last position, GHASH = y_0 H^(n - e_0) + y_1 H^(n - e_1)
+ * (one of the exponents is 0).  ctr 1 = J0 gives the tag mask.  Tables in
+ * LDS: the round-key masks, multiply-by-H and multiply-by-H^8.
+ */
+struct GcmBsLds {
+    uint32_t km[15 * 128]; /* bs_mask_entry layout */
+    uint4 h1[GHASH_TAB_ENTRIES];
+    uint4 h8[GHASH_TAB_ENTRIES];
+    /* each thread's GCM state parked across a group's AES (the AES needs all
+       but ~10 of the 128 VGPRs): y[4], E(J0) words, last position, nonce */
+    uint32_t park[9][256];
+};
+constexpr uint32_t GCM_BS_RECS = 128; /* records per 256-thread workgroup */
+
+NA_DEV void gcm_bs_fill(GcmBsLds &S, const AesCtx *ctx)
+{
+    for (uint32_t e = threadIdx.x; e < 15 * 128; e += blockDim.x) S.km[e] = bs_mask_entry(ctx->rk, e);
+    const uint4 *t1 = (const uint4 *)ctx->tab[0], *t8 = (const uint4 *)ctx->tab8;
+    for (uint32_t i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += blockDim.x) {
+        S.h1[i] = t1[i];
+        S.h8[i] = t8[i];
+    }
+}
+
+/* y <- y * H^k, 0 <= k <= 16 (the context's H^1..H^4 and H^8 tables) */
+NA_DEV void gh_mul_hpow(uint32_t y[4], const AesCtx *ctx, uint32_t k)
+{
+    while (k >= 8) {
+        gh_mul(y, (const uint4 *)ctx->tab8);
+        k -= 8;
+    }
+    if (k >= 4) {
+        gh_mul(y, (const uint4 *)ctx->tab[3]);
+        k -= 4;
+    }
+    if (k) gh_mul(y, (const uint4 *)ctx->tab[k - 1]);
+}
+
+/* 8 bytes at p (8-B aligned), the first nb (0..8) of them */
+NA_DEV void st8(uint8_t *p, uint32_t nb, uint32_t w0, uint32_t w1)
+{
+    if (nb >= 8) {
+        *(uint2 *)p = make_uint2(w0, w1);
+    } else if (nb) {
+        const uint32_t w[4] = {w0, w1, 0u, 0u};
+        store16(p, nb, w);
+    }
+}
+
+/* One record per lane pair.  Returns (open) whether the tag verified; the
+   plaintext is written as it is produced (one pass) and repaired by the
+   caller on a MAC failure. */
+template <bool OPEN>
+NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds &S, const AesCtx *ctx, uint32_t rec0, uint64_t nonce)
+{
+    const uint32_t L = threadIdx.x & 1, tid = threadIdx.x;
+    const uint32_t len = a.len, M = (len + 15) / 16, n = M + 1;
+    const uint32_t NG = (n + 2 + 31) / 32;
+    uint32_t (*park)[256] = S.park;
+    park[0][tid] = 0; park[1][tid] = 0; park[2][tid] = 0; park[3][tid] = 0;
+    park[6][tid] = 0xFFFFFFFFu; /* e: no GHASH position yet */
+    park[7][tid] = (uint32_t)nonce; park[8][tid] = (uint32_t)(nonce >> 32);
+    for (uint32_t g = 0; g < NG; ++g) {
+        uint32_t x[2][32];
+        bs2_ctr_group(S.km, L, park[8][tid], park[7][tid], g, x);
+        if (g == 0) { park[4][tid] = x[0][1]; park[5][tid] = x[1][1]; } /* E(J0) */
+        const uint32_t rec_raw = rec0 + tid / 2;
+        const bool live = rec_raw < a.n_records;
+        const uint32_t rc = live ? rec_raw : a.n_records - 1;
+        const uint8_t *src = a.in + (size_t)rc * a.in_stride;
+        uint8_t *dst = a.out + (size_t)rc * a.out_stride;
+        /* data blocks d = 32g + i - 2: this lane's 8 bytes in, key stream
+           XOR, out; x becomes the CT (the GHASH input), masked to len */
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const int d = (int)(32 * g) + i - 2;
+            if (d < 0 || d >= (int)M) {
+                x[0][i] = x[1][i] = 0;
+                continue;
+            }
+            const uint32_t nb = min(len - 16u * (uint32_t)d, 16u);
+            const uint32_t nbl = nb > 8 * L ? min(nb - 8 * L, 8u) : 0u;
+            const uint2 v = *(const uint2 *)(src + 16 * d + 8 * L); /* FAST: readable */
+            const uint32_t o0 = v.x ^ x[0][i], o1 = v.y ^ x[1][i];
+            if (live) st8(dst + 16 * d + 8 * L, nbl, o0, o1);
+            const uint32_t m0 = nbl >= 4 ? 0xffffffffu : (nbl ? (1u << (8 * nbl)) - 1u : 0u);
+            const uint32_t m1 = nbl >= 8 ? 0xffffffffu : (nbl > 4 ? (1u << (8 * (nbl - 4))) - 1u : 0u);
+            x[0][i] = (OPEN ? v.x : o0) & m0;
+            x[1][i] = (OPEN ? v.y : o1) & m1;
+            if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0); /* a few blocks' loads in flight, not 32 */
+        }
+        /* the length block, position n = slot n + 1 - 32g: BE64(8|AD|) ||
+           BE64(8|CT|), AD empty (lane 1 holds words 2, 3) */
+        if (n + 1 >= 32 * g && n + 1 < 32 * g + 32) {
+            const uint32_t i = n + 1 - 32 * g;
+            const uint64_t cb = (uint64_t)len * 8;
+#pragma unroll
+            for (int q = 0; q < 32; ++q)
+                if ((uint32_t)q == i && L) {
+                    x[0][q] = __builtin_bswap32((uint32_t)(cb >> 32));
+                    x[1][q] = __builtin_bswap32((uint32_t)cb);
+                }
+        }
+        /* whole blocks for the lane's 16 slots 16L + t: lane 0 takes words
+           2, 3 of slots 0..15 from lane 1, lane 1 words 0, 1 of 16..31 */
+        const int first = (int)(32 * g) + 16 * (int)L - 1; /* position of slot 16L */
+        if (first <= (int)n) {
+            uint32_t y[4] = {park[0][tid], park[1][tid], park[2][tid], park[3][tid]};
+            if ((int)park[6][tid] >= 0) { /* jump over the partner's 16 positions: H^16 */
+                gh_mul_lds(y, S.h8);
+                gh_mul_lds(y, S.h8);
+            }
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const uint32_t s0 = L ? x[0][t] : x[0][16 + t], s1 = L ? x[1][t] : x[1][16 + t];
+                const uint32_t r0 = bs_partner(s0), r1 = bs_partner(s1);
+                const int p = first + t;
+                if (p >= 1 && p <= (int)n) {
+                    y[0] ^= L ? r0 : x[0][t];
+                    y[1] ^= L ? r1 : x[1][t];
+                    y[2] ^= L ? x[0][16 + t] : r0;
+                    y[3] ^= L ? x[1][16 + t] : r1;
+                    gh_mul_lds(y, S.h1);
+                }
+            }
+            park[0][tid] = y[0]; park[1][tid] = y[1]; park[2][tid] = y[2]; park[3][tid] = y[3];
+            park[6][tid] = (uint32_t)min((int)n, first + 15);
+        }
+    }
+    /* GHASH = y_0 H^(n - e_0) + y_1 H^(n - e_1) */
+    uint32_t y[4] = {park[0][tid], park[1][tid], park[2][tid], park[3][tid]};
+    gh_mul_hpow(y, ctx, (uint32_t)((int)n - (int)park[6][tid]));
+    uint32_t G[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) G[w] = y[w] ^ bs_partner(y[w]);
+    const uint32_t t0 = G[2 * L] ^ park[4][tid], t1 = G[2 * L + 1] ^ park[5][tid];
+    const uint32_t rec_raw = rec0 + tid / 2;
+    const bool live = rec_raw < a.n_records;
+    const uint32_t rc = live ? rec_raw : a.n_records - 1;
+    if (!OPEN) {
+        if (live) *(uint2 *)(a.out + (size_t)rc * a.out_stride + len + 8 * L) = make_uint2(t0, t1);
+        return true;
+    }
+    const uint2 got = *(const uint2 *)(a.in + (size_t)rc * a.in_stride + len + 8 * L);
+    const uint32_t bad = (got.x ^ t0) | (got.y ^ t1);
+    return (bad | bs_partner(bad)) == 0;
+}
+
+/* In-place repair of a rejected record (MAC failure, one-pass open): its
+   plaintext XORed with the key stream once more is the ciphertext as given
+   (cipher-aesgcm.c:184-186 leaves a rejected buffer untouched). */
+NA_DEV void gcm_bs_repair(const UniformArgs &a, const GcmBsLds &S, uint32_t rc, bool bad, uint64_t nonce)
+{
+    const uint32_t L = threadIdx.x & 1;
+    uint8_t *dst = a.out + (size_t)rc * a.out_stride;
+    const uint32_t len = a.len, M = (len + 15) / 16, n = M + 1, NG = (n + 2 + 31) / 32;
+    for (uint32_t g = 0; g < NG; ++g) {
+        uint32_t x[2][32];
+        bs2_ctr_group(S.km, L, (uint32_t)(nonce >> 32), (uint32_t)nonce, g, x);
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            const int d = (int)(32 * g) + i - 2;
+            if (d < 0 || d >= (int)M || !bad) continue;
+            const uint32_t nb = min(len - 16u * (uint32_t)d, 16u);
+            const uint32_t nbl = nb > 8 * L ? min(nb - 8 * L, 8u) : 0u;
+            const uint2 v = *(const uint2 *)(dst + 16 * d + 8 * L);
+            st8(dst + 16 * d + 8 * L, nbl, v.x ^ x[0][i], v.y ^ x[1][i]);
+        }
+    }
+}
+
+template <bool OPEN>
+NA_DEV void gcm_bs_wg(const UniformArgs &a, GcmBsLds &S, uint32_t blk)
+{
+    const uint32_t rec0 = blk * GCM_BS_RECS;
+    const uint32_t st = rec0 / a.rps; /* one state per workgroup (host-checked) */
+    const AesCtx *ctx = (const AesCtx *)a.keys + st;
+    gcm_bs_fill(S, ctx);
+    __syncthreads();
+    const uint32_t rec_raw = rec0 + threadIdx.x / 2;
+    const bool live = rec_raw < a.n_records;
+    const uint32_t rc = live ? rec_raw : a.n_records - 1;
+    const uint64_t nonce = a.nonce_base[st] + (uint64_t)(rc - st * a.rps);
+    const bool ok = gcm_bs_rec<OPEN>(a, S, ctx, rec0, nonce);
+    if (!OPEN) return;
+    if (live && (threadIdx.x & 1) == 0 && a.status) a.status[rec_raw] = ok ? 0 : 1;
+    const bool bad = live && !ok;
+    if (__ballot(bad) == 0) return;
+    if (a.in == a.out && a.in_stride == a.out_stride) {
+        __threadfence(); /* this wave's plaintext stores, visible to its reads */
+        gcm_bs_repair(a, S, rc, bad, nonce);
+    } else if (bad) {
+        scrub_rejected(a.out + (size_t)rc * a.out_stride, a.in + (size_t)rc * a.in_stride, a.len,
+                       threadIdx.x & 1, 2);
+    }
+}
+
+#define NA_BS_OCC __attribute__((amdgpu_waves_per_eu(4)))
+
+template <bool OPEN>
+__global__ __launch_bounds__(256) NA_BS_OCC void gcm_bs_uniform(UniformArgs a)
+{
+    __shared__ GcmBsLds S;
+    gcm_bs_wg<OPEN>(a, S, blockIdx.x);
+}
+
+#ifndef NA_NO_SETUP_KERNELS /* one definition: launch_aes.hip's (worker.hip includes this file too) */
+/* seal job s and open job o in one launch, workgroups alternating */
+__global__ __launch_bounds__(256) NA_BS_OCC void gcm_bs_duplex(UniformArgs s, UniformArgs o, uint32_t s_blocks,
+                                                               uint32_t o_blocks)
+{
+    __shared__ GcmBsLds S;
+    const uint32_t n = min(s_blocks, o_blocks);
+    uint32_t b = blockIdx.x;
+    bool open;
+    if (b < 2 * n) {
+        open = b & 1;
+        b >>= 1;
+    } else {
+        open = o_blocks > s_blocks;
+        b -= n;
+    }
+    if (open) gcm_bs_wg<true>(o, S, b);
+    else gcm_bs_wg<false>(s, S, b);
+}
+#endif
+
 /* ------------------------------ staged ragged (any mix of states / lengths)
  *
  * 1024-thread workgroups over windows of 256 descriptors, with the same
@@ -1158,6 +1398,56 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
     }
 }
 
+/* GHASH input block i of a record: AD blocks, CT blocks (zero-padded), the
+   lengths block BE64(8|AD|) || BE64(8|CT|) (cipher-aesgcm.c:135-154) */
+NA_DEV void gh_input_block(const uint8_t *ad, uint32_t ad_len, const uint8_t *ct, uint32_t len, uint32_t A,
+                           uint32_t M, uint32_t i, uint32_t x[4])
+{
+    if (i < A) {
+        const uint32_t rem = ad_len - 16 * i;
+        load16(ad + 16 * i, rem >= 16 ? 16u : rem, x);
+    } else if (i < A + M) {
+        const uint32_t b = i - A, rem = len - 16 * b;
+        load16(ct + 16 * b, rem >= 16 ? 16u : rem, x);
+    } else {
+        const uint64_t ab = (uint64_t)ad_len * 8, cb = (uint64_t)len * 8;
+        x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
+        x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
+    }
+}
+
+/* ------------------------------------ row-collaborative GHASH multiply
+ *
+ * y <- y * T for a 128-bit y held (the same) by the 16 lanes of a DPP row:
+ * lane p looks up the two nibble positions of byte p (2p: high nibble, 2p+1:
+ * low) in the 4-bit positional table T, and the row XOR-reduces the 16
+ * partial products by DPP row rotations (8, 4, 2, 1), after which every
+ * lane holds the product.  Two table lookups and ~25 VALU deep instead of
+ * one lane's 32 lookups: the latency form of gh_mul_lds for the single
+ * records of gcm_wide_record (the resident worker's AES-GCM calls). */
+template <int ROR>
+NA_DEV uint32_t row_ror(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + ROR, 0xf, 0xf, false);
+}
+
+NA_DEV void gh_mul_row(uint32_t y[4], const uint4 *tab, uint32_t p)
+{
+    const uint32_t w = p < 4 ? y[0] : (p < 8 ? y[1] : (p < 12 ? y[2] : y[3]));
+    const uint32_t byte = (w >> (8 * (p & 3))) & 255u;
+    const uint4 e = tab[(2 * p) * 16 + (byte >> 4)];
+    const uint4 f = tab[(2 * p + 1) * 16 + (byte & 15u)];
+    uint32_t r[4] = {e.x ^ f.x, e.y ^ f.y, e.z ^ f.z, e.w ^ f.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        r[i] ^= row_ror<8>(r[i]);
+        r[i] ^= row_ror<4>(r[i]);
+        r[i] ^= row_ror<2>(r[i]);
+        r[i] ^= row_ror<1>(r[i]);
+        y[i] = r[i];
+    }
+}
+
 /* ------------------------------------------ wide (small batches, latency)
  *
  * One record per 256-thread workgroup, for batches of at most 512 records
@@ -1169,10 +1459,15 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
  * K-lane Horner (H^K steps, scale by H^(K-l), XOR-reduce; K = 8 with the
  * H^8 table) run by lanes 0..K-1 of wave 0, the table in LDS.
  *   Seal: CTR (and E_K(J0)), then GHASH over the CT just written.
- *   Open: waves 1-3 compute E_K(J0) and the first 191 keystream blocks
- *   while wave 0 runs GHASH; the tag is checked first and the keystream
+ *   Open: the waves GHASH leaves free compute E_K(J0) and the first key
+ *   stream blocks meanwhile; the tag is checked first and the keystream
  *   applied only when it verified (cipher-aesgcm.c:184-186): no plaintext
  *   byte of a rejected record is ever written.
+ * GHASH (table form, round 4): chain l of the K Horner chains runs on DPP
+ * row l (16 lanes, gh_mul_row), so a Horner step is two lookups per lane
+ * and a row reduction instead of 32 lookups on one lane; waves 0-1 hold
+ * the 8 rows, waves 2-3 run the open's early key stream.  The CT form keeps
+ * one lane per chain (gh_mul_ct has no table to spread).
  */
 /* One record on a 256-thread workgroup (the whole workgroup calls it):
    te/sb/hk are the LDS tables (hk: the record's H^K multiply table when not
@@ -1188,7 +1483,10 @@ NA_DEV bool gcm_wide_record(const uint8_t *src, uint8_t *dst, const uint8_t *ad,
 {
     static_assert(K == 4 || K == 8, "GHASH lanes: 4 (H^4) or 8 (H^8)");
 #define NA_GSTAMP(k) do { if (dbg && threadIdx.x == 0) dbg[k] = (uint32_t)__builtin_amdgcn_s_memtime(); } while (0)
-    constexpr uint32_t EARLY = 192; /* open: virtual blocks 0..191 run beside GHASH (waves 1-3) */
+    /* threads running GHASH: K lanes (CT) or K rows of 16 (tables); the
+       others compute the open's first EARLY virtual blocks meanwhile */
+    constexpr uint32_t GH = CT ? 64u : 16u * K;
+    constexpr uint32_t EARLY = 256u - GH;
     const uint32_t t = threadIdx.x, M = (len + 15) / 16;
     const uint32_t *rk = ctx->rk;
     uint32_t ks[4] = {0, 0, 0, 0};
@@ -1207,57 +1505,78 @@ NA_DEV bool gcm_wide_record(const uint8_t *src, uint8_t *dst, const uint8_t *ad,
                 store16(dst + 16 * b, nb, x);
             }
         }
-    } else if (t >= 64) {
-        const uint32_t v = t - 64;
+    } else if (t >= GH) {
+        const uint32_t v = t - GH;
         early = v <= M && v < EARLY;
-        if (dbg && t == 64) dbg[6] = (uint32_t)__builtin_amdgcn_s_memtime();
+        if (dbg && t == GH) dbg[6] = (uint32_t)__builtin_amdgcn_s_memtime();
         if (early) aes_ctr_block(rk, te, sb, nonce, v + 1, ks);
-        if (dbg && t == 64) dbg[7] = (uint32_t)__builtin_amdgcn_s_memtime();
+        if (dbg && t == GH) dbg[7] = (uint32_t)__builtin_amdgcn_s_memtime();
         if (v == 0) { wl[1] = ks[0]; wl[2] = ks[1]; wl[3] = ks[2]; wl[4] = ks[3]; }
     }
     if (!OPEN) __syncthreads(); /* the GHASH lanes read this CT back (same CU) */
     NA_GSTAMP(0);
     uint32_t acc[4] = {0, 0, 0, 0};
-    if (t < (uint32_t)K) {
-        const int l = (int)t;
-        const uint8_t *ct = OPEN ? src : dst;
-        const uint32_t A = (ad_len + 15) / 16, n = A + M + 1;
-        const uint32_t c0 = ((uint32_t)l + n) % K;
-        uint32_t hkn[4] = {0, 0, 0, 0};
-        if constexpr (CT) {
+    const uint8_t *ct = OPEN ? src : dst;
+    const uint32_t A = (ad_len + 15) / 16, n = A + M + 1;
+    if constexpr (CT) {
+        if (t < (uint32_t)K) {
+            const int l = (int)t;
+            const uint32_t c0 = ((uint32_t)l + n) % K;
+            uint32_t hkn[4];
 #pragma unroll
             for (int w = 0; w < 4; ++w) hkn[w] = K == 8 ? ctx->hn8[w] : ctx->hn[K - 1][w];
-        }
-        for (uint32_t i = c0; i < n; i += K) {
-            if (i != c0) {
-                if constexpr (CT) gh_mul_ct(acc, hkn);
-                else gh_mul_lds_lat(acc, hk);
+            for (uint32_t i = c0; i < n; i += K) {
+                if (i != c0) gh_mul_ct(acc, hkn);
+                uint32_t x[4];
+                gh_input_block(ad, ad_len, ct, len, A, M, i, x);
+                gh_to_nat(x);
+                acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
             }
-            uint32_t x[4];
-            if (i < A) {
-                const uint32_t rem = ad_len - 16 * i;
-                load16(ad + 16 * i, rem >= 16 ? 16u : rem, x);
-            } else if (i < A + M) {
-                const uint32_t b = i - A, rem = len - 16 * b;
-                load16(ct + 16 * b, rem >= 16 ? 16u : rem, x);
-            } else {
-                const uint64_t ab = (uint64_t)ad_len * 8, cb = (uint64_t)len * 8;
-                x[0] = __builtin_bswap32((uint32_t)(ab >> 32)); x[1] = __builtin_bswap32((uint32_t)ab);
-                x[2] = __builtin_bswap32((uint32_t)(cb >> 32)); x[3] = __builtin_bswap32((uint32_t)cb);
-            }
-            if constexpr (CT) gh_to_nat(x);
-            acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
+            NA_GSTAMP(1);
+            gh_scale<true, K>(acc, ctx, K - 1 - l);
+#pragma unroll
+            for (int off = 1; off < K; off <<= 1)
+#pragma unroll
+                for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
+            gh_to_nat(acc);
+            NA_GSTAMP(2);
         }
-        NA_GSTAMP(1);
-        gh_scale<CT, K>(acc, ctx, K - 1 - l);
+    } else {
+        if (t < GH) {
+            const uint32_t l = t >> 4, p = t & 15; /* chain l on row l */
+            const uint32_t c0 = (l + n) % K;
+            for (uint32_t i = c0; i < n; i += K) {
+                if (i != c0) gh_mul_row(acc, hk, p);
+                uint32_t x[4];
+                gh_input_block(ad, ad_len, ct, len, A, M, i, x);
+                acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
+            }
+            NA_GSTAMP(1);
+            /* scale by H^(K - l): H^4 first when K - l > 4, then H^(m+1) */
+            uint32_t m = K - 1 - l;
+            if (m >= (uint32_t)GCM_LANES) {
+                gh_mul_row(acc, (const uint4 *)ctx->tab[GCM_LANES - 1], p);
+                m -= GCM_LANES;
+            }
+            gh_mul_row(acc, (const uint4 *)ctx->tab[m], p);
+            if (p == 0) {
 #pragma unroll
-        for (int off = 1; off < K; off <<= 1)
+                for (int w = 0; w < 4; ++w) wl[8 + 4 * l + w] = acc[w];
+            }
+        }
+        __syncthreads();
+        if (t == 0 || t == (uint32_t)K - 1) { /* the rows' sum: open checks on thread 0, seal stores on K-1 */
 #pragma unroll
-            for (int w = 0; w < 4; ++w) acc[w] ^= (uint32_t)__shfl_xor((int)acc[w], off, 64);
-        if constexpr (CT) gh_to_nat(acc);
+            for (int w = 0; w < 4; ++w) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int l = 0; l < K; ++l) v ^= wl[8 + 4 * l + w];
+                acc[w] = v;
+            }
+        }
         NA_GSTAMP(2);
     }
-    if (OPEN) __syncthreads(); /* E_K(J0) from wave 1 */
+    if (OPEN) __syncthreads(); /* E_K(J0) from the early waves */
     NA_GSTAMP(3);
     if (!OPEN) {
         if (t == (uint32_t)K - 1) {
@@ -1278,8 +1597,8 @@ NA_DEV bool gcm_wide_record(const uint8_t *src, uint8_t *dst, const uint8_t *ad,
     __syncthreads();
     NA_GSTAMP(4);
     if (!wl[0]) return false; /* nothing decrypted */
-    if (early && t > 64) { /* keystream block t - 65, computed beside GHASH */
-        const uint32_t b = t - 65, nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
+    if (early && t > GH) { /* keystream block t - GH - 1, computed beside GHASH */
+        const uint32_t b = t - GH - 1, nb = len - 16 * b >= 16 ? 16u : len - 16 * b;
         uint32_t x[4];
         load16(src + 16 * b, nb, x);
 #pragma unroll
@@ -1305,7 +1624,7 @@ __global__ __launch_bounds__(256) void gcm_wide(RaggedArgs a)
 {
     __shared__ uint32_t te[256], sb[256];
     __shared__ uint4 h8[GHASH_TAB_ENTRIES];
-    __shared__ uint32_t wl[5];
+    __shared__ uint32_t wl[40]; /* verdict, E_K(J0), the GHASH rows' sums */
     const uint32_t rec = blockIdx.x, t = threadIdx.x;
     const RecDesc d = a.recs[rec];
     if (reject_len(a, rec, d.len, t == 0)) return; /* uniform over the workgroup */

@@ -115,28 +115,6 @@ static_assert(sizeof(WorkerSlot) == 256, "slot layout");
 #define NA_SYS_LOAD(p) __hip_atomic_load((p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
 #define NA_SYS_STORE(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM)
 
-/* lanes per ChaChaPoly record: one ChaCha block per lane where it fits
-   (a single step), 4..64 */
-NA_DEV uint32_t worker_lanes(uint32_t len)
-{
-    const uint32_t blocks = (len + 63) / 64 + 1;
-    uint32_t k = 4;
-    while (k < 64 && k < blocks) k <<= 1;
-    return k;
-}
-
-template <int K>
-NA_DEV bool worker_chacha(bool open, const RecView &rv)
-{
-    const int lane = (int)(threadIdx.x & 63);
-    if (lane >= K) return true; /* one record: lanes 0..K-1 of wave 0 */
-    if (!open) {
-        seal_il<K, false>(rv, lane);
-        return true;
-    }
-    return open_il<K, false>(rv, lane); /* verify first, then decrypt */
-}
-
 /* ---------------------------------------------- latency-first ChaChaPoly
  *
  * One record on the whole workgroup, built for the depth of its dependency
@@ -152,8 +130,9 @@ NA_DEV bool worker_chacha(bool open, const RecView &rv)
  *    LDS for 64 and 128), then * r: log2(n) multiplies deep;
  *  - open verifies first and writes plaintext only on a match.
  * Records of up to WFAST_BLOCKS - 1 units with n <= 256 take it
- * (worker_fast_fits); the result equals seal_il / open_il's bit for bit (the
- * same Poly1305 value: sum_i b_i r^(n-i+1) mod 2^130-5 + s). */
+ * (worker_fast_fits), longer ones worker_chacha_multi; the result equals
+ * seal_il / open_il's bit for bit (the same Poly1305 value:
+ * sum_i b_i r^(n-i+1) mod 2^130-5 + s). */
 constexpr uint32_t WFAST_BLOCKS = 64; /* ChaCha blocks: 4 lanes each on 256 threads */
 
 NA_DEV bool worker_fast_fits(uint32_t len, uint32_t ad_len)
@@ -343,6 +322,135 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
     return ok;
 }
 
+/* Records past one pass (more than 63 units, or a Poly1305 input of more
+   than 256 blocks): the same layout over P = ceil((J + 1) / 64) ChaCha
+   passes, and G = ceil(n / 256) Poly1305 blocks per lane — lane j runs
+   Horner with r over its G consecutive blocks (right-justified chunks),
+   then the tree of worker_chacha_fast sums the chunks with unit R = r^G:
+     poly = (sum_j h_j R^(NL-1-j)) r,  h_j = sum_k b_(jG+k-pad) r^(G-1-k),
+   which is sum_i b_i r^(n-i+1) again.  Seal XORs each pass into the record
+   in LDS, then authenticates the ciphertext; open authenticates first (pass
+   0 for r and s) and decrypts only a verified record.  A separate
+   instantiation, so records of one pass keep worker_chacha_fast unchanged
+   (round 3 measured a merged version costing them 0.3-0.8 us). */
+template <bool OPEN>
+NA_DEV bool worker_chacha_multi(uint8_t *rec, const uint8_t *ad, uint32_t ad_len, uint32_t len,
+                                const uint8_t *key8, uint64_t nonce, FastLds &F)
+{
+    const int t = (int)threadIdx.x, c = t & 3;
+    const uint32_t q = (uint32_t)t >> 2;
+    const uint64_t c00 = __builtin_amdgcn_s_memtime();
+#define NA_FSTAMP(k) do { if (t == 0) F.dbg[k] = (uint32_t)(__builtin_amdgcn_s_memtime() - c00); } while (0)
+    uint32_t key[8];
+    load_key(key8, key);
+    const uint32_t n_lo = (uint32_t)nonce, n_hi = (uint32_t)(nonce >> 32);
+    const uint32_t J = (len + 63) / 64, P = (J + 1 + 63) / 64; /* blocks 0..J in P passes */
+    /* ChaCha pass p: block v = 64p + q; data words 64(v-1) + 4c + 16i */
+    uint32_t ks0[4] = {0, 0, 0, 0}; /* pass 0 (open: XORed after the verdict) */
+    chacha_quad(key, q, n_lo, n_hi, c, ks0[0], ks0[1], ks0[2], ks0[3]);
+    if (q == 0) { F.rs[c] = ks0[0]; F.rs[4 + c] = ks0[1]; }
+    if (!OPEN) {
+        for (uint32_t p = 0; p < P; ++p) {
+            const uint32_t v = 64 * p + q;
+            uint32_t ks[4];
+            if (p == 0) {
+                ks[0] = ks0[0]; ks[1] = ks0[1]; ks[2] = ks0[2]; ks[3] = ks0[3];
+            } else if (v <= J) {
+                chacha_quad(key, v, n_lo, n_hi, c, ks[0], ks[1], ks[2], ks[3]);
+            }
+            if (v >= 1 && v <= J) {
+                uint32_t *w = (uint32_t *)(rec + 64 * (v - 1) + 4 * c);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[4 * i] ^= ks[i]; /* CT; bytes past len: the tag overwrites */
+            }
+        }
+    }
+    __syncthreads();
+    NA_FSTAMP(0); /* seal: CT in LDS; both: r and s published */
+    const uint32_t a = (ad_len + 15) / 16, m = (len + 15) / 16, n = a + m + 1;
+    const uint32_t G = (n + 255) / 256, NL = (n + G - 1) / G, pad = NL * G - n;
+    const uint32_t N = NL <= 1 ? 1u : 1u << (32 - __builtin_clz(NL - 1));
+    const int j = t - (int)(N - NL); /* this lane's chunk */
+    const Fe r = fe_clamp_r(F.rs[0], F.rs[1], F.rs[2], F.rs[3]);
+    const Mul mr = mk_mul(r);
+    Fe h = fe_zero();
+    if (j >= 0 && (uint32_t)j < NL) {
+        for (uint32_t k = 0; k < G; ++k) {
+            const int idx = j * (int)G + (int)k - (int)pad; /* 0-based block of the Poly input */
+            if (idx < 0) continue;                          /* leading padding of chunk 0 */
+            uint32_t b[4];
+            const uint32_t i = (uint32_t)idx;
+            if (i < a) {
+                lds_block(ad + 16 * i, ad_len - 16 * i, b);
+            } else if (i < a + m) {
+                const uint32_t jj = i - a;
+                lds_block(rec + 16 * jj, len - 16 * jj, b);
+            } else {
+                b[0] = ad_len; b[1] = 0; b[2] = len; b[3] = 0;
+            }
+            h = fe_mul(h, mr);
+            fe_add_block(h, b[0], b[1], b[2], b[3]);
+        }
+    }
+    NA_FSTAMP(1); /* chunks' Horner done */
+    /* R = r^G (G <= 17), square-and-multiply, the same in every lane */
+    Fe R = r;
+    {
+        const int top = 31 - __builtin_clz(G);
+        for (int bit = top - 1; bit >= 0; --bit) {
+            R = fe_mul(R, mk_mul(R));
+            if ((G >> bit) & 1u) R = fe_mul(R, mr);
+        }
+    }
+    Mul mP = mk_mul(R);
+    Fe vv = h;
+    tree_level<1>(vv, mP, t, N, F);
+    tree_level<2>(vv, mP, t, N, F);
+    tree_level<4>(vv, mP, t, N, F);
+    tree_level<8>(vv, mP, t, N, F);
+    tree_level<16>(vv, mP, t, N, F);
+    tree_level<32>(vv, mP, t, N, F);
+    tree_level<64>(vv, mP, t, N, F);
+    tree_level<128>(vv, mP, t, N, F);
+    NA_FSTAMP(2); /* tree done */
+    if (t == 0) {
+        vv = fe_mul(vv, mr);
+        const uint32_t s[4] = {F.rs[4], F.rs[5], F.rs[6], F.rs[7]};
+        uint32_t tag[4];
+        fe_finish(vv, s, tag);
+        if (OPEN) {
+            uint32_t got[4];
+            load16(rec + len, 16, got);
+            F.verdict = tag_equal(tag, got) ? 1u : 0u;
+        } else {
+            store16(rec + len, 16, tag);
+        }
+    }
+    NA_FSTAMP(3); /* tag */
+    if (!OPEN) return true;
+    __syncthreads();
+    const bool ok = F.verdict != 0;
+    if (ok) { /* decrypt the verified record in LDS */
+        for (uint32_t p = 0; p < P; ++p) {
+            const uint32_t v = 64 * p + q;
+            uint32_t ks[4];
+            if (p == 0) {
+                ks[0] = ks0[0]; ks[1] = ks0[1]; ks[2] = ks0[2]; ks[3] = ks0[3];
+            } else if (v <= J) {
+                chacha_quad(key, v, n_lo, n_hi, c, ks[0], ks[1], ks[2], ks[3]);
+            }
+            if (v >= 1 && v <= J) {
+                uint32_t *w = (uint32_t *)(rec + 64 * (v - 1) + 4 * c);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[4 * i] ^= ks[i]; /* bytes past len: not copied out */
+            }
+        }
+    }
+    NA_FSTAMP(4);
+#undef NA_FSTAMP
+    return ok;
+}
+
 /* One 16-byte system-coherent load (a single request: the chunk is read
    whole, never half before and half after the host's 16-byte store). */
 NA_DEV uint4 load_sys16(const uint32_t *p)
@@ -391,7 +499,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
     __shared__ uint32_t cgen[WORKER_CTX_SLOTS], cuse[WORKER_CTX_SLOTS];
     __shared__ uint32_t hdr[16];
     __shared__ uint32_t verdict, s_cmd; /* s_cmd: 0 wait, 1 serve, 2 leave */
-    __shared__ uint32_t wl[5];          /* gcm_wide_record's verdict and E_K(J0) */
+    __shared__ uint32_t wl[40];         /* gcm_wide_record's verdict, E_K(J0), GHASH rows */
     __shared__ uint32_t s_stale;        /* chunks still stamped with an older request */
     __shared__ FastLds fast;
     __shared__ __attribute__((aligned(16))) uint8_t buf[WORKER_DATA];
@@ -531,28 +639,9 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
         if (cipher == NOISE_CIPHER_CHACHAPOLY && worker_fast_fits(len, ad_len)) {
             ok = op ? worker_chacha_fast<true>(rec, ad, ad_len, len, key, nonce, fast)
                     : worker_chacha_fast<false>(rec, ad, ad_len, len, key, nonce, fast);
-        } else if (cipher == NOISE_CIPHER_CHACHAPOLY) {
-            RecView rv;
-            rv.src = rec;
-            rv.dst = rec;
-            rv.ad = ad;
-            rv.key = key;
-            rv.nonce = nonce;
-            rv.len = len;
-            rv.ad_len = ad_len;
-            if (t < 64) {
-                bool r;
-                switch (worker_lanes(len)) {
-                case 4: r = worker_chacha<4>(op, rv); break;
-                case 8: r = worker_chacha<8>(op, rv); break;
-                case 16: r = worker_chacha<16>(op, rv); break;
-                case 32: r = worker_chacha<32>(op, rv); break;
-                default: r = worker_chacha<64>(op, rv); break;
-                }
-                if (t == 0) verdict = r; /* every lane of the group has the verdict */
-            }
-            __syncthreads();
-            ok = verdict != 0;
+        } else if (cipher == NOISE_CIPHER_CHACHAPOLY) { /* past one pass */
+            ok = op ? worker_chacha_multi<true>(rec, ad, ad_len, len, key, nonce, fast)
+                    : worker_chacha_multi<false>(rec, ad, ad_len, len, key, nonce, fast);
         } else {
             const AesCtx *c = (const AesCtx *)cbuf[cs];
             const uint4 *h8 = (const uint4 *)c->tab8;

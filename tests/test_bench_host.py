@@ -49,6 +49,8 @@ def test_default_layout_and_kernel_names():
     its roofline reads from profiles/traffic_<cfg>.json: every name the
     default C2/C3/C4/perf lines look up must be in the committed profile,
     or the line's traffic would silently read null."""
+    import noise_aead as A
+
     assert bench.SLOT_ALIGN == 128
     assert (bench.stride(1400, 128), bench.stride(1416, 128)) == (1408, 1536)
     for cfg in ("c2", "c3", "c4", "perf"):
@@ -56,7 +58,8 @@ def test_default_layout_and_kernel_names():
         n, s = c["records"], c["states"]
         ad = c.get("ad", 0)
         ins, outs = bench.stride(c["len"], 128), bench.stride(c["len"] + 16, 128)
-        k = bench.kernel_name(c["cipher"], n, n // s, 4, ins, outs, c["len"], duplex=True)
+        lanes = A.dev_default_lanes(c["cipher"], n)  # the library's choice, as the bench takes it
+        k = bench.kernel_name(c["cipher"], n, n // s, lanes, ins, outs, c["len"], duplex=True)
         assert "_duplex_" in k, (cfg, k)
         prof = bench.load_pmc(cfg, k)
         assert prof.get("hbm_bytes_per_launch"), (cfg, k)

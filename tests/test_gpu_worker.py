@@ -4,7 +4,8 @@
 the resident worker, not a kernel launch.  ChaChaPoly records of up to 63
 units whose Poly1305 input is at most 256 blocks run the latency-first path
 (four lanes per ChaCha block, a Poly1305 tree over one block per lane);
-longer ones the wave-0 path; AES-GCM gcm_wide_record.  Every case is checked
+longer ones the multi-pass path (P ChaCha passes, G Poly1305 blocks per lane);
+AES-GCM gcm_wide_record.  Every case is checked
 byte for byte against the oracle (the restatement of
 src/backend/ref/cipher-chachapoly.c:107-143 and cipher-aesgcm.c:156-188),
 then opened back, then opened tampered: MAC failure, buffer and nonce left
@@ -22,9 +23,11 @@ pytestmark = pytest.mark.gpu
 CHACHA, AES = 0x4301, 0x4302
 
 # the fast path's edges: one unit, unit boundaries, 63 units (4032 B), and
-# the 256-block Poly limit with a 256-byte AD (3824 B), then the wave-0 path
+# the 256-block Poly limit with a 256-byte AD (3824 B), then the multi-pass
+# path (worker_chacha_multi) up to the 65519-byte maximum
 LENS = [0, 1, 15, 16, 17, 63, 64, 65, 100, 127, 128, 129, 1023, 1024, 1025, 1400,
-        2047, 2048, 3823, 3824, 3825, 4031, 4032, 4033, 4096, 8000, 16384]
+        2047, 2048, 3823, 3824, 3825, 4031, 4032, 4033, 4096, 8000, 16384, 16385, 20000,
+        40001, 65519]
 ADS = [0, 1, 16, 17, 32, 255, 256]
 
 
@@ -33,7 +36,7 @@ def _cases():
     out = []
     for L in LENS:
         for A in ADS:
-            if rnd.random() < 0.5 and L not in (0, 3824, 4032, 4033) and A not in (0, 256):
+            if rnd.random() < 0.5 and L not in (0, 3824, 4032, 4033, 65519) and A not in (0, 256):
                 continue  # a sample of the grid, the edges always
             out.append((L, A))
     return out

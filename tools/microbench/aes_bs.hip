@@ -95,130 +95,8 @@ static void h_encrypt(const uint8_t rk[15][16], uint8_t s[16])
 /* ------------------------------------------------------------ bitsliced */
 struct BsKey { uint32_t m[15][128]; };
 
-/* Boyar-Peralta S-box, x0 = MSB of the byte (in place) */
-NA_DEV void bs_sbox(uint32_t &q0, uint32_t &q1, uint32_t &q2, uint32_t &q3, uint32_t &q4, uint32_t &q5,
-                    uint32_t &q6, uint32_t &q7)
-{
-    const uint32_t x0 = q0, x1 = q1, x2 = q2, x3 = q3, x4 = q4, x5 = q5, x6 = q6, x7 = q7;
-#if BS_FUSED
-    /* the circuit with single-use gates folded into 3-input v_bitop3
-       (84 operations; generated and checked over all 256 inputs) */
-    const uint32_t y14 = __builtin_amdgcn_bitop3_b32(x3, x5, 0u, 0x3c);
-    const uint32_t y13 = __builtin_amdgcn_bitop3_b32(x0, x6, 0u, 0x3c);
-    const uint32_t y9 = __builtin_amdgcn_bitop3_b32(x0, x3, 0u, 0x3c);
-    const uint32_t y8 = __builtin_amdgcn_bitop3_b32(x0, x5, 0u, 0x3c);
-    const uint32_t t0 = __builtin_amdgcn_bitop3_b32(x1, x2, 0u, 0x3c);
-    const uint32_t y1 = __builtin_amdgcn_bitop3_b32(t0, x7, 0u, 0x3c);
-    const uint32_t y4 = __builtin_amdgcn_bitop3_b32(x3, y1, 0u, 0x3c);
-    const uint32_t y12 = __builtin_amdgcn_bitop3_b32(y13, y14, 0u, 0x3c);
-    const uint32_t y2 = __builtin_amdgcn_bitop3_b32(x0, y1, 0u, 0x3c);
-    const uint32_t y5 = __builtin_amdgcn_bitop3_b32(x6, y1, 0u, 0x3c);
-    const uint32_t y3 = __builtin_amdgcn_bitop3_b32(y5, y8, 0u, 0x3c);
-    const uint32_t t1 = __builtin_amdgcn_bitop3_b32(x4, y12, 0u, 0x3c);
-    const uint32_t y15 = __builtin_amdgcn_bitop3_b32(t1, x5, 0u, 0x3c);
-    const uint32_t y20 = __builtin_amdgcn_bitop3_b32(t1, x1, 0u, 0x3c);
-    const uint32_t y6 = __builtin_amdgcn_bitop3_b32(x7, y15, 0u, 0x3c);
-    const uint32_t y10 = __builtin_amdgcn_bitop3_b32(t0, y15, 0u, 0x3c);
-    const uint32_t y11 = __builtin_amdgcn_bitop3_b32(y20, y9, 0u, 0x3c);
-    const uint32_t y7 = __builtin_amdgcn_bitop3_b32(x7, y11, 0u, 0x3c);
-    const uint32_t y17 = __builtin_amdgcn_bitop3_b32(y10, y11, 0u, 0x3c);
-    const uint32_t y19 = __builtin_amdgcn_bitop3_b32(y10, y8, 0u, 0x3c);
-    const uint32_t y16 = __builtin_amdgcn_bitop3_b32(t0, y11, 0u, 0x3c);
-    const uint32_t y21 = __builtin_amdgcn_bitop3_b32(y13, y16, 0u, 0x3c);
-    const uint32_t y18 = __builtin_amdgcn_bitop3_b32(x0, y16, 0u, 0x3c);
-    const uint32_t t2 = __builtin_amdgcn_bitop3_b32(y12, y15, 0u, 0xc0);
-    const uint32_t t4 = __builtin_amdgcn_bitop3_b32(t2, y3, y6, 0x78);
-    const uint32_t t6 = __builtin_amdgcn_bitop3_b32(t2, x7, y4, 0x78);
-    const uint32_t t7 = __builtin_amdgcn_bitop3_b32(y13, y16, 0u, 0xc0);
-    const uint32_t t9 = __builtin_amdgcn_bitop3_b32(t7, y1, y5, 0x78);
-    const uint32_t t11 = __builtin_amdgcn_bitop3_b32(t7, y2, y7, 0x78);
-    const uint32_t t12 = __builtin_amdgcn_bitop3_b32(y11, y9, 0u, 0xc0);
-    const uint32_t t14 = __builtin_amdgcn_bitop3_b32(t12, y14, y17, 0x78);
-    const uint32_t t16 = __builtin_amdgcn_bitop3_b32(t12, y10, y8, 0x78);
-    const uint32_t t21 = __builtin_amdgcn_bitop3_b32(t14, t4, y20, 0x96);
-    const uint32_t t22 = __builtin_amdgcn_bitop3_b32(t16, t6, y19, 0x96);
-    const uint32_t t23 = __builtin_amdgcn_bitop3_b32(t14, t9, y21, 0x96);
-    const uint32_t t24 = __builtin_amdgcn_bitop3_b32(t11, t16, y18, 0x96);
-    const uint32_t t25 = __builtin_amdgcn_bitop3_b32(t21, t22, 0u, 0x3c);
-    const uint32_t t26 = __builtin_amdgcn_bitop3_b32(t21, t23, 0u, 0xc0);
-    const uint32_t t27 = __builtin_amdgcn_bitop3_b32(t24, t26, 0u, 0x3c);
-    const uint32_t t29 = __builtin_amdgcn_bitop3_b32(t22, t25, t27, 0x78);
-    const uint32_t t31 = __builtin_amdgcn_bitop3_b32(t22, t26, 0u, 0x3c);
-    const uint32_t t33 = __builtin_amdgcn_bitop3_b32(t23, t24, t31, 0xe4);
-    const uint32_t t36 = __builtin_amdgcn_bitop3_b32(t24, t27, t33, 0x60);
-    const uint32_t t37 = __builtin_amdgcn_bitop3_b32(t23, t33, t36, 0x96);
-    const uint32_t t39 = __builtin_amdgcn_bitop3_b32(t27, t29, t36, 0x48);
-    const uint32_t t40 = __builtin_amdgcn_bitop3_b32(t25, t39, 0u, 0x3c);
-    const uint32_t t41 = __builtin_amdgcn_bitop3_b32(t37, t40, 0u, 0x3c);
-    const uint32_t t42 = __builtin_amdgcn_bitop3_b32(t29, t33, 0u, 0x3c);
-    const uint32_t t43 = __builtin_amdgcn_bitop3_b32(t29, t40, 0u, 0x3c);
-    const uint32_t t44 = __builtin_amdgcn_bitop3_b32(t33, t37, 0u, 0x3c);
-    const uint32_t t45 = __builtin_amdgcn_bitop3_b32(t41, t42, 0u, 0x3c);
-    const uint32_t z2 = __builtin_amdgcn_bitop3_b32(t33, x7, 0u, 0xc0);
-    const uint32_t z3 = __builtin_amdgcn_bitop3_b32(t43, y16, 0u, 0xc0);
-    const uint32_t z4 = __builtin_amdgcn_bitop3_b32(t40, y1, 0u, 0xc0);
-    const uint32_t z5 = __builtin_amdgcn_bitop3_b32(t29, y7, 0u, 0xc0);
-    const uint32_t z7 = __builtin_amdgcn_bitop3_b32(t45, y17, 0u, 0xc0);
-    const uint32_t z10 = __builtin_amdgcn_bitop3_b32(t37, y3, 0u, 0xc0);
-    const uint32_t z12 = __builtin_amdgcn_bitop3_b32(t43, y13, 0u, 0xc0);
-    const uint32_t z16 = __builtin_amdgcn_bitop3_b32(t45, y14, 0u, 0xc0);
-    const uint32_t t46 = __builtin_amdgcn_bitop3_b32(t42, y9, z16, 0x6a);
-    const uint32_t t47 = __builtin_amdgcn_bitop3_b32(t33, y4, z10, 0x6a);
-    const uint32_t t48 = __builtin_amdgcn_bitop3_b32(t40, y5, z5, 0x6a);
-    const uint32_t t49 = __builtin_amdgcn_bitop3_b32(t44, y12, z10, 0x6a);
-    const uint32_t t52 = __builtin_amdgcn_bitop3_b32(t41, y10, z7, 0x6a);
-    const uint32_t t53 = __builtin_amdgcn_bitop3_b32(t44, y15, z3, 0x6a);
-    const uint32_t t54 = __builtin_amdgcn_bitop3_b32(t42, y11, z7, 0x6a);
-    const uint32_t t55 = __builtin_amdgcn_bitop3_b32(t41, y8, z16, 0x6a);
-    const uint32_t t57 = __builtin_amdgcn_bitop3_b32(t53, z12, z2, 0x96);
-    const uint32_t t58 = __builtin_amdgcn_bitop3_b32(t46, z4, 0u, 0x3c);
-    const uint32_t t59 = __builtin_amdgcn_bitop3_b32(t54, z3, 0u, 0x3c);
-    const uint32_t t61 = __builtin_amdgcn_bitop3_b32(t29, t57, y2, 0x6c);
-    const uint32_t t62 = __builtin_amdgcn_bitop3_b32(t52, t58, 0u, 0x3c);
-    const uint32_t t63 = __builtin_amdgcn_bitop3_b32(t49, t58, 0u, 0x3c);
-    const uint32_t t64 = __builtin_amdgcn_bitop3_b32(t59, z4, 0u, 0x3c);
-    const uint32_t t65 = __builtin_amdgcn_bitop3_b32(t61, t62, 0u, 0x3c);
-    const uint32_t t66 = __builtin_amdgcn_bitop3_b32(t37, t63, y6, 0x6c);
-    const uint32_t s0 = __builtin_amdgcn_bitop3_b32(t59, t63, 0u, 0x3c);
-    const uint32_t s6 = __builtin_amdgcn_bitop3_b32(t48, t62, z12, 0x69);
-    const uint32_t s7 = __builtin_amdgcn_bitop3_b32(t46, t48, t57, 0x69);
-    const uint32_t s3 = __builtin_amdgcn_bitop3_b32(t53, t66, 0u, 0x3c);
-    const uint32_t s4 = __builtin_amdgcn_bitop3_b32(t66, z2, z5, 0x96);
-    const uint32_t s5 = __builtin_amdgcn_bitop3_b32(t47, t65, 0u, 0x3c);
-    const uint32_t s1 = __builtin_amdgcn_bitop3_b32(s3, t64, 0u, 0xc3);
-    const uint32_t s2 = __builtin_amdgcn_bitop3_b32(t55, t64, t65, 0x69);
-#else
-    const uint32_t y14 = x3 ^ x5, y13 = x0 ^ x6, y9 = x0 ^ x3, y8 = x0 ^ x5, t0 = x1 ^ x2;
-    const uint32_t y1 = t0 ^ x7, y4 = y1 ^ x3, y12 = y13 ^ y14, y2 = y1 ^ x0, y5 = y1 ^ x6;
-    const uint32_t y3 = y5 ^ y8, t1 = x4 ^ y12, y15 = t1 ^ x5, y20 = t1 ^ x1, y6 = y15 ^ x7;
-    const uint32_t y10 = y15 ^ t0, y11 = y20 ^ y9, y7 = x7 ^ y11, y17 = y10 ^ y11, y19 = y10 ^ y8;
-    const uint32_t y16 = t0 ^ y11, y21 = y13 ^ y16, y18 = x0 ^ y16;
-    const uint32_t t2 = y12 & y15, t3 = y3 & y6, t4 = t3 ^ t2, t5 = y4 & x7, t6 = t5 ^ t2;
-    const uint32_t t7 = y13 & y16, t8 = y5 & y1, t9 = t8 ^ t7, t10 = y2 & y7, t11 = t10 ^ t7;
-    const uint32_t t12 = y9 & y11, t13 = y14 & y17, t14 = t13 ^ t12, t15 = y8 & y10, t16 = t15 ^ t12;
-    const uint32_t t17 = t4 ^ t14, t18 = t6 ^ t16, t19 = t9 ^ t14, t20 = t11 ^ t16;
-    const uint32_t t21 = t17 ^ y20, t22 = t18 ^ y19, t23 = t19 ^ y21, t24 = t20 ^ y18;
-    const uint32_t t25 = t21 ^ t22, t26 = t21 & t23, t27 = t24 ^ t26, t28 = t25 & t27, t29 = t28 ^ t22;
-    const uint32_t t30 = t23 ^ t24, t31 = t22 ^ t26, t32 = t31 & t30, t33 = t32 ^ t24, t34 = t23 ^ t33;
-    const uint32_t t35 = t27 ^ t33, t36 = t24 & t35, t37 = t36 ^ t34, t38 = t27 ^ t36, t39 = t29 & t38;
-    const uint32_t t40 = t25 ^ t39;
-    const uint32_t t41 = t40 ^ t37, t42 = t29 ^ t33, t43 = t29 ^ t40, t44 = t33 ^ t37, t45 = t42 ^ t41;
-    const uint32_t z0 = t44 & y15, z1 = t37 & y6, z2 = t33 & x7, z3 = t43 & y16, z4 = t40 & y1;
-    const uint32_t z5 = t29 & y7, z6 = t42 & y11, z7 = t45 & y17, z8 = t41 & y10, z9 = t44 & y12;
-    const uint32_t z10 = t37 & y3, z11 = t33 & y4, z12 = t43 & y13, z13 = t40 & y5, z14 = t29 & y2;
-    const uint32_t z15 = t42 & y9, z16 = t45 & y14, z17 = t41 & y8;
-    const uint32_t t46 = z15 ^ z16, t47 = z10 ^ z11, t48 = z5 ^ z13, t49 = z9 ^ z10, t50 = z2 ^ z12;
-    const uint32_t t51 = z2 ^ z5, t52 = z7 ^ z8, t53 = z0 ^ z3, t54 = z6 ^ z7, t55 = z16 ^ z17;
-    const uint32_t t56 = z12 ^ t48, t57 = t50 ^ t53, t58 = z4 ^ t46, t59 = z3 ^ t54, t60 = t46 ^ t57;
-    const uint32_t t61 = z14 ^ t57, t62 = t52 ^ t58, t63 = t49 ^ t58, t64 = z4 ^ t59, t65 = t61 ^ t62;
-    const uint32_t t66 = z1 ^ t63;
-    const uint32_t s0 = t59 ^ t63, s6 = t56 ^ ~t62, s7 = t48 ^ ~t60, t67 = t64 ^ t65;
-    const uint32_t s3 = t53 ^ t66, s4 = t51 ^ t66, s5 = t47 ^ t65, s1 = t64 ^ ~s3, s2 = t55 ^ ~t67;
-#endif
-    q0 = s0; q1 = s1; q2 = s2; q3 = s3; q4 = s4; q5 = s5; q6 = s6; q7 = s7;
-}
-
-NA_DEV uint32_t bs_x3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+/* bs_sbox, bs_x3, bs2_round, bs_partner, bs_transpose32: noise-c_amd/csrc/aes_bs.h
+   (included through aesgcm.hip) */
 
 #define BS_SBOX(q, b) bs_sbox(q[8 * (b)], q[8 * (b) + 1], q[8 * (b) + 2], q[8 * (b) + 3], q[8 * (b) + 4], \
                               q[8 * (b) + 5], q[8 * (b) + 6], q[8 * (b) + 7])
@@ -281,28 +159,6 @@ NA_DEV void bs_round(uint32_t q[128], const uint32_t *m, bool MIX)
     for (int i = 0; i < 128; ++i) q[i] = o[i];
 }
 
-/* swap step of a bit-matrix transpose: exchange a's bits [w, 2w) blocks with
-   b's [0, w) blocks under mask */
-NA_DEV void tswap(uint32_t &a, uint32_t &b, int w, uint32_t mask)
-{
-    const uint32_t t = ((a >> w) ^ b) & mask;
-    b ^= t;
-    a ^= t << w;
-}
-
-/* 32x32 bit transpose of r[0..31] in place: bit i of r[p] <-> bit p of r[i] */
-NA_DEV void transpose32(uint32_t r[32])
-{
-    const uint32_t masks[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-        const int w = 16 >> s;
-#pragma unroll
-        for (int p = 0; p < 32; ++p)
-            if (!(p & w)) tswap(r[p], r[p | w], w, masks[s]);
-    }
-}
-
 /* keystream of the lane's 32 counters ctr0 + i (ctr0 % 32 == 0); MODE 0
    writes them (block-major, 4 LE words each), MODE 1 XOR-accumulates */
 template <int MODE>
@@ -346,7 +202,7 @@ __global__ __launch_bounds__(256) BS_OCC void bs_ctr(const BsKey *__restrict__ K
             for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
                 for (int k = 0; k < 8; ++k) r[8 * rb + (7 - k)] = q[8 * (4 * gw + rb) + k];
-            transpose32(r);
+            bs_transpose32(r);
 #pragma unroll
             for (int i = 0; i < 32; ++i) {
                 if (MODE == 0) out[((size_t)g * 32 + i) * 4 + gw] = r[i];
@@ -369,65 +225,6 @@ __global__ __launch_bounds__(256) BS_OCC void bs_ctr(const BsKey *__restrict__ K
  * is symmetric (both lanes want the partner's (1,0), (2,0), (2,1), (3,1)),
  * one quad_perm [1,0,3,2] DPP per register.  Round-key masks depend on the
  * lane's columns: read from LDS per lane. */
-NA_DEV uint32_t partner(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false); }
-
-/* one round on the lane's half state h[64]; mk: this lane's 64 masks */
-NA_DEV void bs2_round(uint32_t h[64], const uint32_t *mk, bool MIX)
-{
-#pragma unroll
-    for (int b = 0; b < 8; ++b) bs_sbox(h[8 * b], h[8 * b + 1], h[8 * b + 2], h[8 * b + 3], h[8 * b + 4],
-                                       h[8 * b + 5], h[8 * b + 6], h[8 * b + 7]);
-    /* the partner's (1,0), (2,0), (2,1), (3,1): local bytes 1, 2, 6, 7 */
-    uint32_t px[4][8];
-    const int pb[4] = {1, 2, 6, 7};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) px[i][k] = partner(h[8 * pb[i] + k]);
-    uint32_t o[64];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        /* a_r = byte (r, c + r) before ShiftRows, c = 2L + j */
-        const uint32_t *a[4];
-        a[0] = &h[8 * (4 * j + 0)];
-        a[1] = j == 0 ? &h[8 * (4 * 1 + 1)] : px[0];                 /* (1,1) own / (1,0) partner */
-        a[2] = j == 0 ? px[1] : px[2];                               /* (2,0) / (2,1) partner */
-        a[3] = j == 0 ? px[3] : &h[8 * (4 * 0 + 3)];                 /* (3,1) partner / (3,0) own */
-        uint32_t mkc[32];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) mkc[i] = mk[32 * j + i];
-        if (!MIX) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int k = 0; k < 8; ++k) o[8 * (4 * j + r) + k] = a[r][k] ^ mkc[8 * r + k];
-            continue;
-        }
-        uint32_t sx[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sx[k] = bs_x3(a[0][k], a[1][k], a[2][k]) ^ a[3][k];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t *A = a[r], *B = a[(r + 1) & 3];
-            uint32_t t[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) t[k] = A[k] ^ B[k];
-            uint32_t *O = &o[8 * (4 * j + r)];
-            const uint32_t *M = &mkc[8 * r];
-            O[0] = bs_x3(t[1], sx[0], A[0] ^ M[0]);
-            O[1] = bs_x3(t[2], sx[1], A[1] ^ M[1]);
-            O[2] = bs_x3(t[3], sx[2], A[2] ^ M[2]);
-            O[3] = bs_x3(t[4], t[0], bs_x3(sx[3], A[3], M[3]));
-            O[4] = bs_x3(t[5], t[0], bs_x3(sx[4], A[4], M[4]));
-            O[5] = bs_x3(t[6], sx[5], A[5] ^ M[5]);
-            O[6] = bs_x3(t[7], t[0], bs_x3(sx[6], A[6], M[6]));
-            O[7] = bs_x3(t[0], sx[7], A[7] ^ M[7]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 64; ++i) h[i] = o[i];
-}
-
 template <int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void bs2_ctr(
     const BsKey *__restrict__ K, uint32_t n_hi, uint32_t n_lo, uint32_t ctr_base, uint32_t *out, uint64_t *clk)
@@ -464,7 +261,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
 #pragma unroll
     for (int i = 0; i < 64; ++i) h[i] ^= km[0][L][i];
 #pragma unroll 1
-    for (int rr = 1; rr < 15; ++rr) bs2_round(h, km[rr][L], rr < 14);
+    for (int rr = 1; rr < 14; ++rr) bs2_round<true>(h, km[rr][L]);
+    bs2_round<false>(h, km[14][L]);
     uint32_t acc = 0;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -473,7 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void b
         for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
             for (int k = 0; k < 8; ++k) r32[8 * rb + (7 - k)] = h[8 * (4 * j + rb) + k];
-        transpose32(r32);
+        bs_transpose32(r32);
 #pragma unroll
         for (int i = 0; i < 32; ++i) {
             if (MODE == 0) out[((size_t)pair * 32 + i) * 4 + 2 * L + j] = r32[i];
