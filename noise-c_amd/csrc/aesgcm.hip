@@ -957,24 +957,52 @@ __global__ __launch_bounds__(GCM_WG) void gcm_duplex_fused(UniformArgs s, Unifor
  * (one of the exponents is 0).  ctr 1 = J0 gives the tag mask.  Tables in
  * LDS: the round-key masks, multiply-by-H and multiply-by-H^8.
  */
+/* NT threads per workgroup; T8: multiply-by-H as an 8-bit positional table
+   (16 lookups per block instead of 32; 64 KiB, so one 1024-thread
+   workgroup per CU shares it) */
+template <int NT, bool T8>
 struct GcmBsLds {
     uint32_t km[15 * 128]; /* bs_mask_entry layout */
-    uint4 h1[GHASH_TAB_ENTRIES];
+    uint4 h1[T8 ? 16 * 256 : GHASH_TAB_ENTRIES];
     uint4 h8[GHASH_TAB_ENTRIES];
     /* each thread's GCM state parked across a group's AES (the AES needs all
        but ~10 of the 128 VGPRs): y[4], E(J0) words, last position, nonce */
-    uint32_t park[9][256];
+    uint32_t park[9][NT];
 };
-constexpr uint32_t GCM_BS_RECS = 128; /* records per 256-thread workgroup */
+constexpr uint32_t GCM_BS_RECS = 128;   /* records per 256-thread workgroup */
+constexpr uint32_t GCM_BS8_RECS = 512;  /* records per 1024-thread workgroup (8-bit H table) */
 
-NA_DEV void gcm_bs_fill(GcmBsLds &S, const AesCtx *ctx)
+template <int NT, bool T8>
+NA_DEV void gcm_bs_fill(GcmBsLds<NT, T8> &S, const AesCtx *ctx)
 {
-    for (uint32_t e = threadIdx.x; e < 15 * 128; e += blockDim.x) S.km[e] = bs_mask_entry(ctx->rk, e);
+    for (uint32_t e = threadIdx.x; e < 15 * 128; e += NT) S.km[e] = bs_mask_entry(ctx->rk, e);
     const uint4 *t1 = (const uint4 *)ctx->tab[0], *t8 = (const uint4 *)ctx->tab8;
-    for (uint32_t i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += blockDim.x) {
-        S.h1[i] = t1[i];
-        S.h8[i] = t8[i];
+    for (uint32_t i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += NT) S.h8[i] = t8[i];
+    if constexpr (T8) { /* byte position p, value v: the two nibble entries' sum */
+        for (uint32_t e = threadIdx.x; e < 16 * 256; e += NT) {
+            const uint32_t p = e >> 8, v = e & 255;
+            const uint4 hi = t1[(2 * p) * 16 + (v >> 4)], lo = t1[(2 * p + 1) * 16 + (v & 15)];
+            S.h1[e] = make_uint4(hi.x ^ lo.x, hi.y ^ lo.y, hi.z ^ lo.z, hi.w ^ lo.w);
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += NT) S.h1[i] = t1[i];
     }
+}
+
+/* y <- y * Y with Y's 8-bit positional table (byte p of the LE words) */
+NA_DEV void gh_mul_lds8(uint32_t y[4], const uint4 *tab)
+{
+    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+#pragma unroll
+    for (int p = 0; p < 16; p += 2) {
+        const uint32_t b0 = (y[p >> 2] >> (8 * (p & 3))) & 255u;
+        const uint32_t b1 = (y[(p + 1) >> 2] >> (8 * ((p + 1) & 3))) & 255u;
+        const uint4 e = tab[p * 256 + b0];
+        const uint4 f = tab[(p + 1) * 256 + b1];
+        r0 = xor3(r0, e.x, f.x); r1 = xor3(r1, e.y, f.y);
+        r2 = xor3(r2, e.z, f.z); r3 = xor3(r3, e.w, f.w);
+    }
+    y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
 }
 
 /* y <- y * H^k, 0 <= k <= 16 (the context's H^1..H^4 and H^8 tables) */
@@ -1005,13 +1033,13 @@ NA_DEV void st8(uint8_t *p, uint32_t nb, uint32_t w0, uint32_t w1)
 /* One record per lane pair.  Returns (open) whether the tag verified; the
    plaintext is written as it is produced (one pass) and repaired by the
    caller on a MAC failure. */
-template <bool OPEN>
-NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds &S, const AesCtx *ctx, uint32_t rec0, uint64_t nonce)
+template <bool OPEN, int NT, bool T8>
+NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds<NT, T8> &S, const AesCtx *ctx, uint32_t rec0, uint64_t nonce)
 {
     const uint32_t L = threadIdx.x & 1, tid = threadIdx.x;
     const uint32_t len = a.len, M = (len + 15) / 16, n = M + 1;
     const uint32_t NG = (n + 2 + 31) / 32;
-    uint32_t (*park)[256] = S.park;
+    uint32_t (*park)[NT] = S.park;
     park[0][tid] = 0; park[1][tid] = 0; park[2][tid] = 0; park[3][tid] = 0;
     park[6][tid] = 0xFFFFFFFFu; /* e: no GHASH position yet */
     park[7][tid] = (uint32_t)nonce; park[8][tid] = (uint32_t)(nonce >> 32);
@@ -1075,7 +1103,8 @@ NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds &S, const AesCtx *ctx, uin
                     y[1] ^= L ? r1 : x[1][t];
                     y[2] ^= L ? x[0][16 + t] : r0;
                     y[3] ^= L ? x[1][16 + t] : r1;
-                    gh_mul_lds(y, S.h1);
+                    if constexpr (T8) gh_mul_lds8(y, S.h1);
+                    else gh_mul_lds(y, S.h1);
                 }
             }
             park[0][tid] = y[0]; park[1][tid] = y[1]; park[2][tid] = y[2]; park[3][tid] = y[3];
@@ -1104,7 +1133,8 @@ NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds &S, const AesCtx *ctx, uin
 /* In-place repair of a rejected record (MAC failure, one-pass open): its
    plaintext XORed with the key stream once more is the ciphertext as given
    (cipher-aesgcm.c:184-186 leaves a rejected buffer untouched). */
-NA_DEV void gcm_bs_repair(const UniformArgs &a, const GcmBsLds &S, uint32_t rc, bool bad, uint64_t nonce)
+template <int NT, bool T8>
+NA_DEV void gcm_bs_repair(const UniformArgs &a, const GcmBsLds<NT, T8> &S, uint32_t rc, bool bad, uint64_t nonce)
 {
     const uint32_t L = threadIdx.x & 1;
     uint8_t *dst = a.out + (size_t)rc * a.out_stride;
@@ -1124,10 +1154,10 @@ NA_DEV void gcm_bs_repair(const UniformArgs &a, const GcmBsLds &S, uint32_t rc, 
     }
 }
 
-template <bool OPEN>
-NA_DEV void gcm_bs_wg(const UniformArgs &a, GcmBsLds &S, uint32_t blk)
+template <bool OPEN, int NT, bool T8>
+NA_DEV void gcm_bs_wg(const UniformArgs &a, GcmBsLds<NT, T8> &S, uint32_t blk)
 {
-    const uint32_t rec0 = blk * GCM_BS_RECS;
+    const uint32_t rec0 = blk * (NT / 2);
     const uint32_t st = rec0 / a.rps; /* one state per workgroup (host-checked) */
     const AesCtx *ctx = (const AesCtx *)a.keys + st;
     gcm_bs_fill(S, ctx);
@@ -1155,16 +1185,24 @@ NA_DEV void gcm_bs_wg(const UniformArgs &a, GcmBsLds &S, uint32_t blk)
 template <bool OPEN>
 __global__ __launch_bounds__(256) NA_BS_OCC void gcm_bs_uniform(UniformArgs a)
 {
-    __shared__ GcmBsLds S;
+    __shared__ GcmBsLds<256, false> S;
+    gcm_bs_wg<OPEN>(a, S, blockIdx.x);
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(1024) NA_BS_OCC void gcm_bs8_uniform(UniformArgs a)
+{
+    __shared__ GcmBsLds<1024, true> S;
     gcm_bs_wg<OPEN>(a, S, blockIdx.x);
 }
 
 #ifndef NA_NO_SETUP_KERNELS /* one definition: launch_aes.hip's (worker.hip includes this file too) */
 /* seal job s and open job o in one launch, workgroups alternating */
-__global__ __launch_bounds__(256) NA_BS_OCC void gcm_bs_duplex(UniformArgs s, UniformArgs o, uint32_t s_blocks,
-                                                               uint32_t o_blocks)
+template <int NT, bool T8>
+__global__ __launch_bounds__(NT) NA_BS_OCC void gcm_bs_duplex(UniformArgs s, UniformArgs o, uint32_t s_blocks,
+                                                              uint32_t o_blocks)
 {
-    __shared__ GcmBsLds S;
+    __shared__ GcmBsLds<NT, T8> S;
     const uint32_t n = min(s_blocks, o_blocks);
     uint32_t b = blockIdx.x;
     bool open;
