@@ -490,8 +490,13 @@ def main():
     payload_step = 2.0 * N * L * world                         # both directions, all ranks
     value = payload_step * args.steps / elapsed / GIB
     alg_seal = N * (2 * L + 16 + AD) + len(wl.sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
-    # a VERIFY_FIRST open never shares the duplex launch: two launches a step
-    two_launch = wl.duplex and args.verify_first
+    # a VERIFY_FIRST open shares the duplex launch only with the one-lane
+    # ChaChaPoly and the staged AES-GCM kernels (aead_api.hip run_duplex);
+    # otherwise a step is two launches
+    vf_duplex = "_duplex_" in kernel_name(wl.cipher, N, wl.sh["rps"], wl.lanes, wl.in_stride,
+                                          wl.out_stride, L, True, args.ct_ghash) and \
+        (wl.cipher == AES or wl.lanes == 1)
+    two_launch = wl.duplex and args.verify_first and not vf_duplex
     kname = kernel_name(wl.cipher, N, wl.sh["rps"], wl.lanes, wl.in_stride, wl.out_stride, L,
                         wl.duplex and not two_launch, args.ct_ghash)
     if two_launch:
@@ -505,7 +510,8 @@ def main():
     else:
         alg_launch, launch_ms_ = alg_seal, seal_ms
     achieved = alg_launch / (launch_ms_ * 1e-3) / 1e9
-    pmc = load_pmc(args.config, kname, 1.0 / world if cfg.get("strong") else 1.0)
+    # the committed PMC profiles are of the default (one-pass) open order
+    pmc = {} if args.verify_first else load_pmc(args.config, kname, 1.0 / world if cfg.get("strong") else 1.0)
     traffic = pmc.get("hbm_bytes_per_launch")
     S_all = S * world
     result = {

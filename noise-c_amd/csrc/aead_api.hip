@@ -78,9 +78,7 @@ bool solo_enabled()
 int uniform_lanes(const NoiseAeadUniform *j, bool open)
 {
     if (j->lanes_per_record) return (int)j->lanes_per_record;
-    if (j->n_records >= SOLO_MIN_RECORDS && solo_enabled() && uniform_fast(j, open) &&
-        !verify_first(j, open))
-        return 1;
+    if (j->n_records >= SOLO_MIN_RECORDS && solo_enabled() && uniform_fast(j, open)) return 1;
     return auto_lanes(j->n_records, 0);
 }
 
@@ -269,19 +267,19 @@ int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform
         }
         if (clash) return NOISE_ERROR_INVALID_PARAM;
     }
-    /* a VERIFY_FIRST open never shares a launch with the one-pass kernels */
-    if (verify_first(oj, true)) {
-        rc = run_uniform(cipher_id, sj, stream, false);
-        if (!rc) rc = run_uniform(cipher_id, oj, stream, true);
-        return rc;
-    }
+    /* a VERIFY_FIRST open shares a launch only with kernels that run its
+       order: the one-lane ChaChaPoly open (AUTH + DEC passes) and the staged
+       AES-GCM open (GHASH, verdict, then CTR) */
+    const bool vf = verify_first(oj, true);
+    UniformArgs oa = to_args(oj);
+    oa.vf = vf;
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY && sj->n_records && oj->n_records) {
         const int ks = uniform_lanes(sj, false), ko = uniform_lanes(oj, true);
         const bool us = (ks >= 4 || ks == 1) && sj->recs_per_state % (64u / (uint32_t)ks) == 0;
         const bool uo = (ko >= 4 || ko == 1) && oj->recs_per_state % (64u / (uint32_t)ko) == 0;
-        if (ks == ko && (ks == 1 || ks == 4 || ks == 8) && us == uo && uniform_fast(sj, false) &&
+        if (ks == ko && (ks == 1 || ((ks == 4 || ks == 8) && !vf)) && us == uo && uniform_fast(sj, false) &&
             uniform_fast(oj, true)) {
-            return chacha_duplex(to_args(sj), to_args(oj), ks, us, (hipStream_t)stream);
+            return chacha_duplex(to_args(sj), oa, ks, us, (hipStream_t)stream);
         }
     }
     if (cipher_id == NOISE_CIPHER_AESGCM && sj->n_records && oj->n_records &&
@@ -292,7 +290,7 @@ int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform
         ct_ghash(sj->flags) == ct_ghash(oj->flags)) {
         rc = hip_rc(ensure_aes_tables());
         if (rc) return rc;
-        return aes_duplex(to_args(sj), to_args(oj), ct_ghash(sj->flags), (hipStream_t)stream);
+        return aes_duplex(to_args(sj), oa, ct_ghash(sj->flags), (hipStream_t)stream);
     }
     rc = run_uniform(cipher_id, sj, stream, false);
     if (!rc) rc = run_uniform(cipher_id, oj, stream, true);

@@ -1087,9 +1087,12 @@ NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds<NT, T8> &S, const AesCtx *
         /* whole blocks for the lane's 16 slots 16L + t: lane 0 takes words
            2, 3 of slots 0..15 from lane 1, lane 1 words 0, 1 of 16..31 */
         const int first = (int)(32 * g) + 16 * (int)L - 1; /* position of slot 16L */
-        if (first <= (int)n) {
+        /* pair-uniform (the DPP exchange reads the partner lane, which must
+           be active); the lane's own Horner only where it holds positions */
+        if ((int)(32 * g) - 1 <= (int)n) {
+            const bool mine = first <= (int)n;
             uint32_t y[4] = {park[0][tid], park[1][tid], park[2][tid], park[3][tid]};
-            if ((int)park[6][tid] >= 0) { /* jump over the partner's 16 positions: H^16 */
+            if (mine && (int)park[6][tid] >= 0) { /* jump over the partner's 16 positions: H^16 */
                 gh_mul_lds(y, S.h8);
                 gh_mul_lds(y, S.h8);
             }
@@ -1098,7 +1101,7 @@ NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds<NT, T8> &S, const AesCtx *
                 const uint32_t s0 = L ? x[0][t] : x[0][16 + t], s1 = L ? x[1][t] : x[1][16 + t];
                 const uint32_t r0 = bs_partner(s0), r1 = bs_partner(s1);
                 const int p = first + t;
-                if (p >= 1 && p <= (int)n) {
+                if (mine && p >= 1 && p <= (int)n) {
                     y[0] ^= L ? r0 : x[0][t];
                     y[1] ^= L ? r1 : x[1][t];
                     y[2] ^= L ? x[0][16 + t] : r0;
@@ -1107,8 +1110,10 @@ NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds<NT, T8> &S, const AesCtx *
                     else gh_mul_lds(y, S.h1);
                 }
             }
-            park[0][tid] = y[0]; park[1][tid] = y[1]; park[2][tid] = y[2]; park[3][tid] = y[3];
-            park[6][tid] = (uint32_t)min((int)n, first + 15);
+            if (mine) {
+                park[0][tid] = y[0]; park[1][tid] = y[1]; park[2][tid] = y[2]; park[3][tid] = y[3];
+                park[6][tid] = (uint32_t)min((int)n, first + 15);
+            }
         }
     }
     /* GHASH = y_0 H^(n - e_0) + y_1 H^(n - e_1) */

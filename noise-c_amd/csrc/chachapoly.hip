@@ -1268,17 +1268,25 @@ NA_DEV SoloRec solo_rec(const UniformArgs &a, uint32_t wave_job)
    (hipcc waits before an LDS read for the youngest LDS-DMA; reading the tile
    after issuing the next DMA, as the 4-lane kernels do, made every step wait
    for the DMA it had just issued and serialised the stores behind it.) */
-template <bool OPEN>
+/* solo_pass modes: SEAL and OPEN1 (one-pass open) as above; the
+   verify-first open runs AUTH (Poly1305 over the CT, nothing written) and
+   then DEC over the verified records (key stream only; stores gated by
+   okm, the owners' verdicts per coalesced instruction, and ok). */
+enum SoloMode { SOLO_SEAL, SOLO_OPEN1, SOLO_AUTH, SOLO_DEC };
+
+template <int MODE>
 NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const uint32_t key[8],
-                      const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, const R32 &r, P32 &h)
+                      const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, const R32 &r, P32 &h,
+                      uint32_t okm = 0xffu, bool ok = true)
 {
+    constexpr bool STORES = MODE != SOLO_AUTH, KEYSTREAM = MODE != SOLO_AUTH, POLY = MODE != SOLO_DEC;
     for (uint32_t m = 0; m < q.S; ++m) {
         uint4 *cur = tiles + SOLO_TILE * (m & 1), *nxt = tiles + SOLO_TILE * ((m + 1) & 1);
         uint32_t wu[2][16];
         solo_wait();
         solo_get(cur, q.lane, 0, wu[0]);
         solo_get(cur, q.lane, 1, wu[1]);
-        if (m >= 1) solo_store(a, q.rec0, q.lane, m - 1, q.full_lim, nxt, 0xffu);
+        if (STORES && m >= 1) solo_store(a, q.rec0, q.lane, m - 1, q.full_lim, nxt, okm);
         __builtin_amdgcn_wave_barrier();
         if (m + 1 < q.S) solo_dma(a, q.rec0, q.lane, m + 1, q.lim, nxt);
         /* Two waves share a SIMD and the older one takes the issue slots:
@@ -1286,25 +1294,29 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
            second finished alone, at one wave's issue rate.  A wave that is
            ahead lowers its priority (aead_device.h): C2 +5-8 %, C4 +0.5 %
            (profiles/r04/solo_prio_ab.jsonl). */
-        prio_by_progress(m, q.S);
+        if (KEYSTREAM) prio_by_progress(m, q.S);
 #ifdef NA_SOLO_X2
         uint32_t xs[2][16];
-        if (2 * m + 1 < q.J) chacha20_2block_pre(key, pre, 2 * m + 1, 2 * m + 2, n_lo, n_hi, xs[0], xs[1]);
-        else chacha20_block_pre(key, pre, 2 * m + 1, n_lo, n_hi, xs[0]);
+        if (KEYSTREAM) {
+            if (2 * m + 1 < q.J) chacha20_2block_pre(key, pre, 2 * m + 1, 2 * m + 2, n_lo, n_hi, xs[0], xs[1]);
+            else chacha20_block_pre(key, pre, 2 * m + 1, n_lo, n_hi, xs[0]);
+        }
 #endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u; /* unit, ChaCha block j + 1 */
             if (j < q.J) {
                 uint32_t x[16], w[16];
+                if constexpr (KEYSTREAM) {
 #ifdef NA_SOLO_X2
 #pragma unroll
-                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
+                    for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
 #else
-                chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+                    chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
 #endif
+                }
                 uint32_t nb = 4;
-                if constexpr (OPEN) {
+                if constexpr (MODE == SOLO_OPEN1 || MODE == SOLO_AUTH) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) w[i] = wu[u][i];
                     if (j == q.J - 1) { /* bytes past len are never stored */
@@ -1312,26 +1324,30 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
                         nb = (q.tail + 15) / 16;
                     }
                     p32_unit(h, r, w, nb);
+                    if constexpr (MODE == SOLO_OPEN1) {
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-                    if (j == q.J - 1 && q.live) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
+                        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+                        if (j == q.J - 1 && q.live) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
+                    }
                 } else {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) w[i] = wu[u][i] ^ x[i];
                     if (j == q.J - 1) {
-                        if (q.live) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
-                        mask_unit(w, q.tail);
-                        nb = (q.tail + 15) / 16;
+                        if (q.live && ok) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
+                        if (POLY) {
+                            mask_unit(w, q.tail);
+                            nb = (q.tail + 15) / 16;
+                        }
                     }
-                    p32_unit(h, r, w, nb);
+                    if constexpr (POLY) p32_unit(h, r, w, nb);
                 }
-                solo_put(cur, q.lane, u, w);
+                if constexpr (STORES) solo_put(cur, q.lane, u, w);
             }
         }
     }
-    if (q.S) {
+    if (STORES && q.S) {
         __builtin_amdgcn_wave_barrier();
-        solo_store(a, q.rec0, q.lane, q.S - 1, q.full_lim, tiles + SOLO_TILE * ((q.S - 1) & 1), 0xffu);
+        solo_store(a, q.rec0, q.lane, q.S - 1, q.full_lim, tiles + SOLO_TILE * ((q.S - 1) & 1), okm);
     }
 }
 
@@ -1348,7 +1364,7 @@ NA_DEV void seal_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
     uint32_t s[4];
     P32 h;
     solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, q.rc) : nullptr, a.ad_len, r, s, h);
-    solo_pass<false>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
+    solo_pass<SOLO_SEAL>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
     uint32_t tag[4];
     solo_tag(h, r, a.ad_len, q.len, s, tag);
     if (q.live) tag_out(u_dst(a, q.rc) + q.len, q.len, tag);
@@ -1357,7 +1373,11 @@ NA_DEV void seal_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
 /* Open, one pass: Poly1305 over each ciphertext unit as it arrives, then
    the plaintext out; a wave holding a rejected record repairs it after the
    verdict exactly as open_il_staged does (in place: XOR with the key stream
-   once more; out of place: zeroed). */
+   once more; out of place: zeroed).  VERIFY_FIRST (a.vf, the reference's
+   order, cipher-chachapoly.c:135-141): an AUTH pass over the wave's records,
+   the verdicts, then a DEC pass writing only verified records — a rejected
+   record's output is never written.  The DEC pass reads the ciphertext
+   again, mostly from L2 / MALL (a wave's 64 records are ~90 KB). */
 template <bool UKEY>
 NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_job)
 {
@@ -1374,12 +1394,24 @@ NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
     uint32_t s[4];
     P32 h;
     solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, rc) : nullptr, a.ad_len, r, s, h);
-    solo_pass<true>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
+    if (a.vf) solo_pass<SOLO_AUTH>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
+    else solo_pass<SOLO_OPEN1>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
     uint32_t tag[4], got[4];
     solo_tag(h, r, a.ad_len, len, s, tag);
     tag_in<true>(u_src(a, rc), len, got); /* the tag bytes are never written */
     const bool ok = tag_equal(tag, got);
     if (live && a.status) a.status[rec_raw] = ok ? 0 : 1;
+    if (a.vf) {
+        if (__ballot(live && ok) == 0) return;
+        uint32_t okm = 0; /* bit i: the owner coalesced instruction i serves verified */
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            okm |= (__shfl((int)ok, (int)(8u * i + (lane >> 3)), 64) != 0 ? 1u : 0u) << i;
+        __builtin_amdgcn_wave_barrier(); /* the AUTH pass's tile reads are done */
+        if (S) solo_dma(a, rec0, lane, 0, lim, tiles);
+        solo_pass<SOLO_DEC>(a, q, tiles, key, pre, n_lo, n_hi, r, h, okm, ok);
+        return;
+    }
     const bool bad = live && !ok;
     if (__ballot(bad) == 0) return; /* wave-uniform: the common case */
 
@@ -1773,16 +1805,27 @@ __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_open_solo(UniformA
 
 /* chachapoly_duplex_staged's two-job launch over the one-lane kernels */
 template <bool UKEY>
+/* chunk C > 0: the paired blocks go in runs of C, seal and open runs
+   alternating (C = the CU count: the dispatcher hands each CU one block of
+   the seal run and one of the open run, so a SIMD's two waves are one seal
+   and one open); C = 0: blocks alternate one by one (then block b and
+   block b + #CUs, which share a CU, are the same kind). */
 __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_duplex_solo(
-    UniformArgs s, UniformArgs o, uint32_t s_blocks, uint32_t o_blocks)
+    UniformArgs s, UniformArgs o, uint32_t s_blocks, uint32_t o_blocks, uint32_t C)
 {
     __shared__ uint4 tiles[4][2 * SOLO_TILE];
     const uint32_t n = min(s_blocks, o_blocks);
+    const uint32_t full = C ? n / C * C : 0; /* pairs placed in whole runs */
     uint32_t b = blockIdx.x;
     bool open;
-    if (b < 2 * n) {
+    if (b < 2 * full) {
+        const uint32_t run = b / C;
+        open = run & 1;
+        b = (run >> 1) * C + b % C;
+    } else if (b < 2 * n) {
+        b -= 2 * full;
         open = b & 1;
-        b >>= 1;
+        b = full + (b >> 1);
     } else {
         open = o_blocks > s_blocks;
         b -= n;

@@ -35,15 +35,16 @@ KernelFn<UniformArgs> chacha_staged_fn(bool open, bool ukey)
     return open ? chachapoly_open_staged<K, false> : chachapoly_seal_staged<K, false>;
 }
 
-/* vf: a VERIFY_FIRST open takes the two-pass chachapoly_open_uniform, never
-   the one-pass staged kernel */
+/* vf: a VERIFY_FIRST open takes the one-lane kernel's AUTH + DEC passes
+   (open_solo_staged) or the two-pass chachapoly_open_uniform, never the
+   one-pass 4/8-lane staged kernels */
 template <bool FAST>
 KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf)
 {
     switch (k) {
     case 1:
         /* one lane per record, LDS-staged (seal_solo_staged) */
-        if (FAST && !(open && vf)) {
+        if (FAST) {
             if (ukey) return open ? chachapoly_open_solo<true> : chachapoly_seal_solo<true>;
             return open ? chachapoly_open_solo<false> : chachapoly_seal_solo<false>;
         }
@@ -161,18 +162,40 @@ int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, bool ukey,
     return launch(fn, a.n_records, k, a, s);
 }
 
+/* chachapoly_duplex_solo's run length: the device's CU count (one seal and
+   one open block per CU); NOISE_AEAD_DUPLEX_RUNS=0 alternates block by
+   block (A/B runs) */
+static uint32_t duplex_run_chunk()
+{
+    static const uint32_t c = [] {
+        const char *e = getenv("NOISE_AEAD_DUPLEX_RUNS");
+        if (e && e[0] == '0') return 0u;
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return 0u;
+        return (uint32_t)cus;
+    }();
+    return c;
+}
+
 int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, hipStream_t s)
 {
-    if (duplex_persist()) {
+    if (duplex_persist() && k != 1) {
         if (k == 4) return ukey ? duplex_persist_launch<4, true>(a, b, s) : duplex_persist_launch<4, false>(a, b, s);
         if (k == 8) return ukey ? duplex_persist_launch<8, true>(a, b, s) : duplex_persist_launch<8, false>(a, b, s);
         return NOISE_ERROR_INVALID_PARAM;
     }
     const uint32_t sb = (uint32_t)(((uint64_t)a.n_records * k + 255) / 256);
     const uint32_t ob = (uint32_t)(((uint64_t)b.n_records * k + 255) / 256);
+    if (k == 1) {
+        worker_park_for_batch(sb + ob);
+        hipLaunchKernelGGL(ukey ? chachapoly_duplex_solo<true> : chachapoly_duplex_solo<false>, dim3(sb + ob),
+                           dim3(256), 0, s, a, b, sb, ob, duplex_run_chunk());
+        return hip_rc(hipGetLastError());
+    }
     void (*fn)(UniformArgs, UniformArgs, uint32_t, uint32_t);
-    if (k == 1) fn = ukey ? chachapoly_duplex_solo<true> : chachapoly_duplex_solo<false>;
-    else if (k == 4) fn = ukey ? chachapoly_duplex_staged<4, true> : chachapoly_duplex_staged<4, false>;
+    if (k == 4) fn = ukey ? chachapoly_duplex_staged<4, true> : chachapoly_duplex_staged<4, false>;
     else if (k == 8) fn = ukey ? chachapoly_duplex_staged<8, true> : chachapoly_duplex_staged<8, false>;
     else return NOISE_ERROR_INVALID_PARAM;
     worker_park_for_batch(sb + ob);

@@ -82,6 +82,7 @@ class NoiseAeadRagged(C.Structure):
 
 FLAG_FAST = 1
 FLAG_CT_GHASH = 2
+FLAG_VERIFY_FIRST = 4
 _LIB = None
 
 

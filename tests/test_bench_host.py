@@ -122,3 +122,18 @@ def test_shard_goldens_cover_every_rank():
         base = json.load(f)["configs"]
     assert bench.shard_golden("c2", 0, 1, False) == base["c2"]["sealed_sha256"]
     assert bench.shard_golden("c4", 0, 1, True) == base["c4"]["sealed_sha256"]
+
+
+def test_bench_module_constants_exist():
+    """Every noise_aead constant bench.py reads (A.FLAG_*, A.CHACHA ...) is
+    defined: a run with a flag whose constant is missing would die on the GPU
+    box after its setup, not here."""
+    import re
+
+    import noise_aead as A
+
+    with open(os.path.join(ROOT, "bench.py")) as f:
+        names = set(re.findall(r"\bA\.([A-Z][A-Z0-9_]+)\b", f.read()))
+    assert names, "no constants found"
+    missing = sorted(n for n in names if not hasattr(A, n))
+    assert not missing, missing

@@ -162,8 +162,9 @@ def test_c5_shard_digest_on_gpu(rank):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,lanes", [("c2", 0), ("c2", 4), ("c3", 0)])
-def test_full_size_duplex_at_bench_slots(name, lanes):
+@pytest.mark.parametrize("name,lanes,vf", [("c2", 0, False), ("c2", 4, False), ("c3", 0, False),
+                                           ("c2", 0, True), ("c3", 0, True)])
+def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     """The kernels bench.py times: C2 / C3 at full size
     through noise_aead_dev_duplex_uniform at the bench's 128-B record slots
     (in_stride 1408, out_stride 1536), one state, recs_per_state 65 536 —
@@ -172,7 +173,9 @@ def test_full_size_duplex_at_bench_slots(name, lanes):
     half's sealed records hash to the golden digest (cipher-chachapoly.c
     :107-133 / cipher-aesgcm.c:156-170 bytes); the open half, over a batch
     sealed beforehand with 64 records tampered, accepts every other record
-    with the plaintext digest and rejects (zeroes) exactly the tampered ones."""
+    with the plaintext digest and rejects (zeroes) exactly the tampered ones.
+    vf: the open half with NOISE_AEAD_FLAG_VERIFY_FIRST (the bench's
+    --verify-first line, still one launch): rejected records never written."""
     import torch
 
     import noise_aead as A
@@ -207,7 +210,7 @@ def test_full_size_duplex_at_bench_slots(name, lanes):
     st = torch.full((N,), 9, dtype=torch.uint8, device="cuda")
     sj = A.uniform_job(inp=pt.data_ptr(), out=ct_a.data_ptr(), in_stride=ins, out_stride=outs, **common)
     oj = A.uniform_job(inp=ct_b.data_ptr(), out=back.data_ptr(), in_stride=outs, out_stride=ins,
-                       status=st.data_ptr(), **common)
+                       status=st.data_ptr(), flags=4 if vf else 0, **common)
     assert A.dev_duplex(cipher, sj, oj, sp) == 0
     torch.cuda.synchronize()
     sealed = ct_a.view(N, outs)[:, :L + 16].contiguous().cpu().numpy()
@@ -221,4 +224,6 @@ def test_full_size_duplex_at_bench_slots(name, lanes):
     good = torch.ones(N, dtype=torch.bool, device="cuda")
     good[torch.from_numpy(bad).to("cuda")] = False
     assert torch.equal(bv[good], pv[good])
-    assert int(bv[~good].max().item()) == 0  # rejected records zeroed out of place
+    # rejected records: zeroed out of place (one pass) / never written (verify-first)
+    assert int(bv[~good].max().item()) == (0xA5 if vf else 0)
+    assert int(bv[~good].min().item()) == (0xA5 if vf else 0)

@@ -245,14 +245,17 @@ SLOT_CASES = [((1400, 1024, 512), (1400, 768, 256)), ((1400, 512, 256), (1024, 2
     (CHACHA, 1, "fast", 0), (CHACHA, 1, "slot128", 0), (CHACHA, 0, "slot128", 0),
     (CHACHA, 4, "slot128", 0), (CHACHA, 8, "slot128", 0), (AES, 0, "slot128", 0),
     (AES, 0, "slot128", FLAG_CT_GHASH), (CHACHA, 4, "slot128", FLAG_VERIFY_FIRST),
-    (AES, 0, "slot128", FLAG_VERIFY_FIRST)])
+    (AES, 0, "slot128", FLAG_VERIFY_FIRST), (CHACHA, 1, "slot128", FLAG_VERIFY_FIRST),
+    (CHACHA, 1, "fast", FLAG_VERIFY_FIRST)])
 def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout, flags):
     """noise_aead_dev_duplex_uniform: seal job A and open job B (other keys,
     nonces, length, record count; some records tampered) in one call must
     equal the two separate calls — i.e. the oracle — byte for byte.  ChaCha
     FAST layouts run the one-launch chachapoly_duplex_staged kernel; AES-GCM
     with one state per 256 records runs gcm_duplex_fused (plain and CT
-    GHASH); the others, and a VERIFY_FIRST open, two launches.  A rejected
+    GHASH); a VERIFY_FIRST open shares the launch with the one-lane ChaCha
+    kernel (AUTH + DEC passes) and the AES duplex kernels, the others run two
+    launches.  A rejected
     record's output is zeroed (one-pass opens) or never written
     (VERIFY_FIRST)."""
     torch = _torch()
@@ -874,3 +877,83 @@ def test_interleaved_slots_one_buffer(aead, gpu, oracle, cipher):
     for i in range(count):
         o = 2 * slot * i
         assert np.array_equal(back[o:o + L], pt[o:o + L]), i
+
+
+@pytest.mark.parametrize("flags", [0, FLAG_VERIFY_FIRST])
+def test_duplex_solo_runs(aead, gpu, oracle, flags):
+    """chachapoly_duplex_solo places the paired blocks in runs of the CU count
+    (seal run, open run, ...) and the remainder block by block: job sizes
+    that leave a partial run and a partial last block (300 x 256 + 17 seal
+    records, 290 x 256 + 5 open records, one lane each).  The duplex output
+    equals the separate launches byte for byte (both orders of open), and
+    sampled records — every run boundary's neighbours among them — equal
+    the oracle; tampered records are rejected."""
+    torch = _torch()
+    rng = np.random.default_rng(977 + flags)
+    L, rps = 40, 64
+    na, nb_ = 300 * 256 + 17, 290 * 256 + 5
+    ins, outs = 64, 64
+    Sa, Sb = (na + rps - 1) // rps, (nb_ + rps - 1) // rps
+    ka = rng.integers(0, 256, (Sa, 32), dtype=np.uint8)
+    kb = rng.integers(0, 256, (Sb, 32), dtype=np.uint8)
+    nba = rng.integers(0, 2**62, Sa, dtype=np.uint64)
+    nbb = rng.integers(0, 2**62, Sb, dtype=np.uint64)
+    pta = rng.integers(0, 256, na * ins + 64, dtype=np.uint8)
+    ptb = rng.integers(0, 256, nb_ * ins + 64, dtype=np.uint8)
+    ctxa, _k1 = prepare(aead, CHACHA, ka)
+    ctxb, _k2 = prepare(aead, CHACHA, kb)
+    d_nba, d_nbb = dev(nba.view(np.int64)), dev(nbb.view(np.int64))
+    d_pta, d_ptb = dev(pta), dev(ptb)
+    # batch B sealed by the separate (oracle-checked) kernel, then tampered
+    d_ctb = torch.full((nb_ * outs + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+    assert aead.dev_uniform(False, CHACHA, ctx=ctxb.data_ptr(), nonce_base=d_nbb.data_ptr(),
+                            inp=d_ptb.data_ptr(), out=d_ctb.data_ptr(), in_stride=ins, out_stride=outs,
+                            length=L, n_records=nb_, recs_per_state=rps, lanes=1, stream=stream()) == 0
+    bad = np.unique(rng.integers(0, nb_, 40))
+    flat = d_ctb.view(-1)
+    flat[torch.from_numpy(bad * outs + rng.integers(0, L + 16, len(bad))).to("cuda")] ^= 0x20
+    # separate launches: the expected bytes
+    exp_a = torch.full((na * outs + 64,), 0x11, dtype=torch.uint8, device="cuda")
+    exp_b = torch.full((nb_ * ins + 64,), 0x22, dtype=torch.uint8, device="cuda")
+    exp_st = torch.full((nb_,), 7, dtype=torch.uint8, device="cuda")
+    assert aead.dev_uniform(False, CHACHA, ctx=ctxa.data_ptr(), nonce_base=d_nba.data_ptr(),
+                            inp=d_pta.data_ptr(), out=exp_a.data_ptr(), in_stride=ins, out_stride=outs,
+                            length=L, n_records=na, recs_per_state=rps, lanes=1, stream=stream()) == 0
+    assert aead.dev_uniform(True, CHACHA, ctx=ctxb.data_ptr(), nonce_base=d_nbb.data_ptr(),
+                            inp=d_ctb.data_ptr(), out=exp_b.data_ptr(), in_stride=outs, out_stride=ins,
+                            length=L, n_records=nb_, recs_per_state=rps, status=exp_st.data_ptr(),
+                            lanes=1, flags=flags, stream=stream()) == 0
+    got_a = torch.full_like(exp_a, 0x11)
+    got_b = torch.full_like(exp_b, 0x22)
+    got_st = torch.full_like(exp_st, 7)
+    sj = aead.uniform_job(ctx=ctxa.data_ptr(), nonce_base=d_nba.data_ptr(), inp=d_pta.data_ptr(),
+                          out=got_a.data_ptr(), in_stride=ins, out_stride=outs, length=L,
+                          n_records=na, recs_per_state=rps, lanes=1)
+    oj = aead.uniform_job(ctx=ctxb.data_ptr(), nonce_base=d_nbb.data_ptr(), inp=d_ctb.data_ptr(),
+                          out=got_b.data_ptr(), in_stride=outs, out_stride=ins, length=L,
+                          n_records=nb_, recs_per_state=rps, status=got_st.data_ptr(), lanes=1,
+                          flags=flags)
+    assert aead.dev_duplex(CHACHA, sj, oj, stream()) == 0
+    sync()
+    assert torch.equal(got_a, exp_a)
+    assert torch.equal(got_b, exp_b)
+    assert torch.equal(got_st, exp_st)
+    st = got_st.cpu().numpy()
+    exp = np.zeros(nb_, dtype=np.uint8)
+    exp[bad] = 1
+    assert np.array_equal(st, exp)
+    # sampled records against the oracle: every 997th plus the neighbours
+    # of each 256-block run boundary (records 65536k - 1, 65536k)
+    sample = sorted(set(list(range(0, na, 997)) + [na - 1] +
+                        [r for k in range(1, na // 65536 + 1) for r in (65536 * k - 1, 65536 * k)
+                         if r < na]))
+    ga = got_a.cpu().numpy()
+    for i in sample:
+        s_ = i // rps
+        ct = oracle.encrypt(CHACHA, bytes(ka[s_]), int(nba[s_]) + i % rps,
+                            bytes(pta[i * ins:i * ins + L]), b"")
+        assert bytes(ga[i * outs:i * outs + L + 16]) == ct, i
+    gb = got_b.cpu().numpy()
+    for i in range(0, nb_, 991):
+        if i not in bad:
+            assert np.array_equal(gb[i * ins:i * ins + L], ptb[i * ins:i * ins + L]), i

@@ -23,7 +23,7 @@ REC_DT = [("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "
 
 
 @pytest.mark.parametrize("cipher,lanes,rps", [(CHACHA, 4, 256), (CHACHA, 8, 256), (CHACHA, 4, 13),
-                                              (CHACHA, 1, 16), (CHACHA, 64, 16), (AES, 0, 256),
+                                              (CHACHA, 1, 16), (CHACHA, 1, 64), (CHACHA, 64, 16), (AES, 0, 256),
                                               (AES, 0, 13)])
 @pytest.mark.parametrize("in_place", [False, True])
 def test_uniform_verify_first(aead, gpu, oracle, cipher, lanes, rps, in_place):
