@@ -235,8 +235,10 @@ int noise_aead_dev_open_uniform(int cipher_id, const NoiseAeadUniform *job, void
  * overlap anything the other job reads (records, AD) or writes, else
  * NOISE_ERROR_INVALID_PARAM.  Either job may have n_records == 0.  When the
  * two jobs cannot share a kernel (unaligned layouts, different lane counts,
- * AESGCM without one state per 256 records, a VERIFY_FIRST open) the library
- * issues the two launches on `stream` instead. */
+ * AESGCM without one state per 256 records, a VERIFY_FIRST ChaChaPoly open
+ * on 4 or 8 lanes per record) the library issues the two launches on
+ * `stream` instead; a VERIFY_FIRST open on one lane per record (the default
+ * from 65 536 records) or on the staged AES-GCM kernel keeps the one launch. */
 int noise_aead_dev_duplex_uniform(int cipher_id, const NoiseAeadUniform *seal_job,
                                   const NoiseAeadUniform *open_job, void *stream);
 

@@ -1461,34 +1461,50 @@ NA_DEV void gh_input_block(const uint8_t *ad, uint32_t ad_len, const uint8_t *ct
 
 /* ------------------------------------ row-collaborative GHASH multiply
  *
- * y <- y * T for a 128-bit y held (the same) by the 16 lanes of a DPP row:
- * lane p looks up the two nibble positions of byte p (2p: high nibble, 2p+1:
- * low) in the 4-bit positional table T, and the row XOR-reduces the 16
- * partial products by DPP row rotations (8, 4, 2, 1), after which every
- * lane holds the product.  Two table lookups and ~25 VALU deep instead of
- * one lane's 32 lookups: the latency form of gh_mul_lds for the single
- * records of gcm_wide_record (the resident worker's AES-GCM calls). */
-template <int ROR>
-NA_DEV uint32_t row_ror(uint32_t v)
+ * A 16-lane DPP row multiplies one GHASH value by a table T, each lane
+ * holding ONE byte of the value: lane p looks up the two nibble positions of
+ * byte p (2p: high nibble, 2p+1: low) in the 4-bit positional table T, and
+ * the 16 partial products (128 bits each) are reduce-scattered so that lane
+ * p ends with byte p of the product — exactly what its next lookups index.
+ * Partners: p ^ 8 (row_ror 8: words 0-1 vs 2-3), 7 - p within the half
+ * (row_half_mirror: differs in bit 2, keeps the word), p ^ 2 and p ^ 1
+ * (quad_perm: the 16-bit half, the byte); the four partner sets together
+ * cover all 16 lanes.  Two lookups, 5 DPP moves and ~20 VALU per multiply
+ * instead of one lane's 32 lookups: the latency form of gh_mul_lds for the
+ * single records of gcm_wide_record (the resident worker's AES-GCM calls). */
+template <int CTRL>
+NA_DEV uint32_t dpp_mov(uint32_t v)
 {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x120 + ROR, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
 }
 
-NA_DEV void gh_mul_row(uint32_t y[4], const uint4 *tab, uint32_t p)
+NA_DEV uint32_t gh_mul_row_byte(uint32_t yb, const uint4 *tab, uint32_t p)
 {
-    const uint32_t w = p < 4 ? y[0] : (p < 8 ? y[1] : (p < 12 ? y[2] : y[3]));
-    const uint32_t byte = (w >> (8 * (p & 3))) & 255u;
-    const uint4 e = tab[(2 * p) * 16 + (byte >> 4)];
-    const uint4 f = tab[(2 * p + 1) * 16 + (byte & 15u)];
-    uint32_t r[4] = {e.x ^ f.x, e.y ^ f.y, e.z ^ f.z, e.w ^ f.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        r[i] ^= row_ror<8>(r[i]);
-        r[i] ^= row_ror<4>(r[i]);
-        r[i] ^= row_ror<2>(r[i]);
-        r[i] ^= row_ror<1>(r[i]);
-        y[i] = r[i];
+    const uint4 e = tab[(2 * p) * 16 + (yb >> 4)];
+    const uint4 f = tab[(2 * p + 1) * 16 + (yb & 15u)];
+    const bool hi = p & 8, b2 = p & 4;
+    /* lanes p < 8 keep words 0-1, p >= 8 words 2-3; each sends the partner's */
+    const uint32_t k0 = hi ? e.z ^ f.z : e.x ^ f.x, k1 = hi ? e.w ^ f.w : e.y ^ f.y;
+    const uint32_t s0 = hi ? e.x ^ f.x : e.z ^ f.z, s1 = hi ? e.y ^ f.y : e.w ^ f.w;
+    const uint32_t a0 = k0 ^ dpp_mov<0x128>(s0), a1 = k1 ^ dpp_mov<0x128>(s1); /* row_ror 8 */
+    const uint32_t w = (b2 ? a1 : a0) ^ dpp_mov<0x141>(b2 ? a0 : a1);          /* row_half_mirror */
+    const uint32_t v = w ^ dpp_mov<0x4E>(w);                                   /* quad_perm [2,3,0,1] */
+    const uint32_t h = (p & 2) ? v >> 16 : v & 0xffffu;
+    const uint32_t u = h ^ dpp_mov<0xB1>(h);                                   /* quad_perm [1,0,3,2] */
+    return (p & 1) ? (u >> 8) & 255u : u & 255u;
+}
+
+/* byte p of GHASH input block i (gh_input_block's bytes, memory order) */
+NA_DEV uint32_t gh_input_byte(const uint8_t *ad, uint32_t ad_len, const uint8_t *ct, uint32_t len, uint32_t A,
+                              uint32_t M, uint32_t i, uint32_t p)
+{
+    if (i < A) return 16 * i + p < ad_len ? ad[16 * i + p] : 0u;
+    if (i < A + M) {
+        const uint32_t o = 16 * (i - A) + p;
+        return o < len ? ct[o] : 0u;
     }
+    const uint64_t bits = p < 8 ? (uint64_t)ad_len * 8 : (uint64_t)len * 8;
+    return (uint32_t)(bits >> (8 * (7 - (p & 7)))) & 255u;
 }
 
 /* ------------------------------------------ wide (small batches, latency)
@@ -1507,9 +1523,10 @@ NA_DEV void gh_mul_row(uint32_t y[4], const uint4 *tab, uint32_t p)
  *   applied only when it verified (cipher-aesgcm.c:184-186): no plaintext
  *   byte of a rejected record is ever written.
  * GHASH (table form, round 4): chain l of the K Horner chains runs on DPP
- * row l (16 lanes, gh_mul_row), so a Horner step is two lookups per lane
- * and a row reduction instead of 32 lookups on one lane; waves 0-1 hold
- * the 8 rows, waves 2-3 run the open's early key stream.  The CT form keeps
+ * row l (16 lanes, one byte of the value each, gh_mul_row_byte), so a
+ * Horner step is two lookups per lane and a 5-move reduce-scatter instead
+ * of 32 lookups on one lane; waves 0-1 hold the 8 rows, waves 2-3 run the
+ * open's early key stream.  The CT form keeps
  * one lane per chain (gh_mul_ct has no table to spread).
  */
 /* One record on a 256-thread workgroup (the whole workgroup calls it):
@@ -1586,26 +1603,28 @@ NA_DEV bool gcm_wide_record(const uint8_t *src, uint8_t *dst, const uint8_t *ad,
         }
     } else {
         if (t < GH) {
-            const uint32_t l = t >> 4, p = t & 15; /* chain l on row l */
+            const uint32_t l = t >> 4, p = t & 15; /* chain l on row l, byte p on lane p */
             const uint32_t c0 = (l + n) % K;
+            uint32_t yb = 0;
             for (uint32_t i = c0; i < n; i += K) {
-                if (i != c0) gh_mul_row(acc, hk, p);
-                uint32_t x[4];
-                gh_input_block(ad, ad_len, ct, len, A, M, i, x);
-                acc[0] ^= x[0]; acc[1] ^= x[1]; acc[2] ^= x[2]; acc[3] ^= x[3];
+                const uint32_t xb = gh_input_byte(ad, ad_len, ct, len, A, M, i, p);
+                if (i != c0) yb = gh_mul_row_byte(yb, hk, p);
+                yb ^= xb;
             }
             NA_GSTAMP(1);
-            /* scale by H^(K - l): H^4 first when K - l > 4, then H^(m+1) */
+            /* scale by H^(K - l): H^K itself (hk), else H^4 first when
+               K - l > 4, then H^(m+1) */
             uint32_t m = K - 1 - l;
-            if (m >= (uint32_t)GCM_LANES) {
-                gh_mul_row(acc, (const uint4 *)ctx->tab[GCM_LANES - 1], p);
-                m -= GCM_LANES;
+            if (m == (uint32_t)K - 1) {
+                yb = gh_mul_row_byte(yb, hk, p);
+            } else {
+                if (m >= (uint32_t)GCM_LANES) {
+                    yb = gh_mul_row_byte(yb, (const uint4 *)ctx->tab[GCM_LANES - 1], p);
+                    m -= GCM_LANES;
+                }
+                yb = gh_mul_row_byte(yb, (const uint4 *)ctx->tab[m], p);
             }
-            gh_mul_row(acc, (const uint4 *)ctx->tab[m], p);
-            if (p == 0) {
-#pragma unroll
-                for (int w = 0; w < 4; ++w) wl[8 + 4 * l + w] = acc[w];
-            }
+            ((uint8_t *)(wl + 8 + 4 * l))[p] = (uint8_t)yb;
         }
         __syncthreads();
         if (t == 0 || t == (uint32_t)K - 1) { /* the rows' sum: open checks on thread 0, seal stores on K-1 */

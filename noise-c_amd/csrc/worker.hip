@@ -498,7 +498,7 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
     __shared__ uint64_t ctag[WORKER_CTX_SLOTS]; /* host address of the cached context */
     __shared__ uint32_t cgen[WORKER_CTX_SLOTS], cuse[WORKER_CTX_SLOTS];
     __shared__ uint32_t hdr[16];
-    __shared__ uint32_t verdict, s_cmd; /* s_cmd: 0 wait, 1 serve, 2 leave */
+    __shared__ uint32_t s_cmd;          /* 0 wait, 1 serve, 2 leave */
     __shared__ uint32_t wl[40];         /* gcm_wide_record's verdict, E_K(J0), GHASH rows */
     __shared__ uint32_t s_stale;        /* chunks still stamped with an older request */
     __shared__ FastLds fast;

@@ -24,6 +24,7 @@ b c5 --config c5 --steps 10 --warmup 2 --no-cpu-baseline
 b perf --config perf --steps 20 --warmup 5
 b c2_verify_first --steps 20 --warmup 5 --verify-first --no-cpu-baseline
 b c3_verify_first --config c3 --steps 20 --warmup 5 --verify-first --no-cpu-baseline
+b c5_verify_first --config c5 --steps 10 --warmup 2 --verify-first --no-cpu-baseline
 : > $O/latency.jsonl
 for c in chachapoly aesgcm; do
   for n in 64 1024 1400 16384 65519; do
