@@ -127,7 +127,9 @@ def test_batch_beside_resident_worker(gpu):
                           .strip().splitlines()[-1])
     print("parked", parked["ratio"], "unparked", unparked["ratio"])
     assert max(parked["resident_before_warm"]) >= 1  # the single call did leave a worker
-    assert parked["ratio"] <= 1.05, parked
+    # cold batches of 0.11 ms vary by +-5 % between launches: 1.10 separates
+    # parked (measured 1.04-1.05) from unparked (1.36-1.43)
+    assert parked["ratio"] <= 1.10, parked
 
 
 def _tool(name):

@@ -59,7 +59,7 @@ def main():
     lib = A.lib()
     lib.noise_aead_debug_workers_resident.restype = int
     cold, warm, resident_before = [], [], []
-    for r in range(8):
+    for r in range(12):
         # cold: no worker (the last one has idled out: 2 ms without requests)
         t0 = time.time()
         while lib.noise_aead_debug_workers_resident() and time.time() - t0 < 1.0:
