@@ -29,9 +29,10 @@
  * sets `exiting` and looks at seq once more, so a request posted meanwhile
  * is either served or seen by the host (exiting set, done behind): the host
  * then waits for the stream and starts a new worker at the same seq.  A
- * device runs up to kWorkersPerDev workers, each with its own slot and
- * stream: a calling thread takes a free one without waiting (its own first),
- * so N threads on N CipherStates make N calls at once, as on the CPU.  Batch
+ * device runs up to workers_per_dev() workers (one per high-priority
+ * hardware queue: 4 by default), each with its own slot and stream: a
+ * calling thread takes a free one without waiting (its own first), so N
+ * threads on N CipherStates make up to that many calls at once.  Batch
  * launches that fill every CU ask the resident workers to leave first
  * (worker_park_for_batch), so no batch workgroup waits for a worker's CU.
  *
@@ -482,7 +483,10 @@ NA_DEV uint4 load_sys16_raw(const uint8_t *p)
 }
 
 /* polls without a request after which only the header is polled: 20 us */
-constexpr uint64_t POLL_BACKOFF = 2000;
+#ifndef NA_POLL_BACKOFF
+#define NA_POLL_BACKOFF 2000
+#endif
+constexpr uint64_t POLL_BACKOFF = NA_POLL_BACKOFF;
 
 /* 256 threads.  req: the header chunks (4 in host memory; 8 in device
    memory, vram); in: the stream's stamped chunks, tail: the rest raw; last:
@@ -723,6 +727,38 @@ constexpr int kMaxDev = 64;
    its own (a workgroup on its own CU, launched on first use and gone 2 ms
    after its last request), claimed without waiting while one is free. */
 constexpr int kWorkersPerDev = 8;
+
+/* A resident worker never ends while calls keep coming (up to LIFETIME), so
+   it must own its hardware queue: a kernel queued behind it on the same AQL
+   queue waits for it to leave.  HIP maps streams onto GPU_MAX_HW_QUEUES
+   queues per device and priority (4 by default), so the workers run on
+   high-priority streams — a pool apart from the application's normal
+   streams (tools/queue_probe.cpp: a memset on a new normal stream waited
+   the worker's whole 5 s lifetime beside a normal-priority worker, 20-60 us
+   beside high-priority ones) — and a device runs at most as many workers
+   as that pool has queues, so no two workers share one.  More concurrent
+   workers: raise GPU_MAX_HW_QUEUES (up to kWorkersPerDev are used).
+   NOISE_AEAD_WORKER_PRIO=normal / low: the A/B placements. */
+int worker_stream_prio()
+{
+    static const int v = [] {
+        const char *e = getenv("NOISE_AEAD_WORKER_PRIO");
+        if (!e) return 1;
+        return !strcmp(e, "normal") ? 0 : (!strcmp(e, "low") ? -1 : 1);
+    }();
+    return v;
+}
+
+int workers_per_dev()
+{
+    static const int v = [] {
+        const char *e = getenv("GPU_MAX_HW_QUEUES");
+        int q = e ? atoi(e) : 4;
+        if (q < 1) q = 4;
+        return q < kWorkersPerDev ? q : kWorkersPerDev;
+    }();
+    return v;
+}
 Worker g_worker[kMaxDev][kWorkersPerDev];
 std::atomic<uint32_t> g_next_pref{0};
 thread_local int t_pref = -1;             /* this thread's first-choice worker */
@@ -828,7 +864,15 @@ int worker_setup(Worker &w, int dev)
         w.in = w.din = (uint4 *)((uint8_t *)w.vbase + 128);
         w.tail = w.dtail = (uint8_t *)(w.in + WORKER_SPEC);
     }
-    if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess) return -1;
+    if (worker_stream_prio() == 0) {
+        if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess) return -1;
+    } else {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return -1;
+        if (hipStreamCreateWithPriority(&w.stream, hipStreamNonBlocking,
+                                        worker_stream_prio() > 0 ? greatest : least) != hipSuccess)
+            return -1;
+    }
     std::call_once(g_atexit_once, [] { atexit(worker_stop_all); });
     w.state = 1;
     return 1;
@@ -884,17 +928,18 @@ int worker_launch(Worker &w)
    (set up failed on all of them). */
 Worker *claim_worker(int dev, std::unique_lock<std::mutex> &lk)
 {
-    if (t_pref < 0) t_pref = (int)(g_next_pref.fetch_add(1, std::memory_order_relaxed) % kWorkersPerDev);
-    for (int i = 0; i < kWorkersPerDev; ++i) {
-        Worker &w = g_worker[dev][(t_pref + i) % kWorkersPerDev];
+    const int nw = workers_per_dev();
+    if (t_pref < 0) t_pref = (int)(g_next_pref.fetch_add(1, std::memory_order_relaxed) % (uint32_t)nw);
+    for (int i = 0; i < nw; ++i) {
+        Worker &w = g_worker[dev][(t_pref + i) % nw];
         std::unique_lock<std::mutex> l(w.mu, std::try_to_lock);
         if (!l.owns_lock()) continue;
         if (worker_setup(w, dev) != 1) continue;
         lk = std::move(l);
         return &w;
     }
-    for (int i = 0; i < kWorkersPerDev; ++i) {
-        Worker &w = g_worker[dev][(t_pref + i) % kWorkersPerDev];
+    for (int i = 0; i < nw; ++i) {
+        Worker &w = g_worker[dev][(t_pref + i) % nw];
         std::unique_lock<std::mutex> l(w.mu);
         if (worker_setup(w, dev) != 1) continue;
         lk = std::move(l);

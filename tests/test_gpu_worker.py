@@ -145,19 +145,40 @@ def test_single_calls_scale_over_threads(gpu):
     takes a resident worker of its own, as T CPU threads would each run the
     reference's cipherstate.c:293-410 without a lock): 8 threads reach at
     least 4x the call rate of one (tools/mt_calls: 1400-B encrypt + decrypt
-    per iteration, every record checked)."""
+    per iteration, every record checked).  One worker per high-priority
+    hardware queue: GPU_MAX_HW_QUEUES=8 gives the 8 threads 8 workers (the
+    HIP default of 4 caps the device at 4)."""
     import json
     tool = _tool("mt_calls")
     rates = {}
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
     for t in (1, 8):
         r = subprocess.run([tool, "chachapoly", str(t), "1400", "1.0"], timeout=60,
-                           capture_output=True, text=True)
+                           capture_output=True, text=True, env=env)
         assert r.returncode == 0, r.stdout + r.stderr
         d = json.loads(r.stdout.strip().splitlines()[-1])
         assert d["ok"]
         rates[t] = d["calls_per_s"]
     print("calls/s", rates)
     assert rates[8] >= 4 * rates[1], rates
+
+
+def test_other_streams_beside_resident_workers(gpu):
+    """Work the application queues on its own streams does not wait for the
+    resident workers: with 1 and 4 threads making single calls back to back,
+    a memset on each of 8 newly created streams completes in well under a
+    millisecond (tools/queue_probe).  A worker on a normal-priority stream
+    shares a hardware queue with such streams and held them for its whole
+    5 s lifetime; the workers' high-priority streams keep them apart."""
+    import json
+    tool = _tool("queue_probe")
+    for workers in (1, 4):
+        r = subprocess.run([tool, "8", str(workers)], timeout=60, capture_output=True, text=True)
+        assert r.returncode == 0, r.stdout + r.stderr
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        print(d)
+        assert d["calls"] > 0
+        assert max(d["memset_us"]) < 20000, d
 
 
 def test_worker_launch_failure_falls_back(gpu):
