@@ -185,18 +185,21 @@ int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_
  *       receives CT || tag (len + 16 bytes).
  * open: in + i*in_stride holds CT || tag; status[i] = 0 (ok) or 1 (MAC
  *       failure).  A verified record's len plaintext bytes go to
- *       out + i*out_stride.  A rejected record, by default:
- *         - in place: its CT || tag read back exactly as given;
- *         - out of place: its len output bytes are ZEROED.
- *       The default opens decrypt as they authenticate (one pass over the
- *       ciphertext), so until the kernel ends a rejected record's output
- *       bytes may transiently hold unauthenticated plaintext; the kernel
- *       undoes it (restores / zeroes) before it completes.  With
- *       NOISE_AEAD_FLAG_VERIFY_FIRST the open authenticates first and writes
- *       a record's output only after its tag verified — the order of the
- *       reference's ref backends (cipher-chachapoly.c:135-141,
- *       cipher-aesgcm.c:172-188): a rejected record's output is not written
- *       at all, not even zeroed.
+ *       out + i*out_stride.  Open order:
+ *         - AESGCM opens always authenticate first and write a record's
+ *           output only after its tag verified — the order of the
+ *           reference's ref backends (cipher-aesgcm.c:172-188): a rejected
+ *           record's output is not written at all (in place: CT || tag read
+ *           back as given; out of place: the output bytes keep whatever
+ *           they held).  It costs nothing there.
+ *         - CHACHAPOLY opens by default decrypt as they authenticate (one
+ *           pass over the ciphertext), and a rejected record reads back in
+ *           place exactly as given, out of place as ZEROED output bytes;
+ *           until the kernel ends its output bytes may transiently hold
+ *           unauthenticated plaintext, which the kernel undoes (restores /
+ *           zeroes) before it completes.  With NOISE_AEAD_FLAG_VERIFY_FIRST
+ *           they take the reference's order (cipher-chachapoly.c:135-141),
+ *           as AESGCM does, at 15-20 % of the batch rate.
  * Memory: input and output records must be either exactly in place
  * (in == out and in_stride == out_stride) or disjoint record by record:
  * with one stride for both sides the records may interleave (input and
@@ -298,8 +301,9 @@ typedef struct NoiseAeadRagged {
 /* Open only: authenticate first, decrypt only a verified record, and write
  * nothing for a rejected one (the reference's verify-then-decrypt order,
  * cipher-chachapoly.c:135-141, cipher-aesgcm.c:172-188).  Without it the
- * FAST-layout opens decrypt in one pass and undo a rejected record's
- * plaintext before the kernel ends (see the uniform open above).  The host
+ * FAST-layout ChaChaPoly opens decrypt in one pass and undo a rejected
+ * record's plaintext before the kernel ends (see the uniform open above);
+ * AESGCM opens take this order whether or not it is set.  The host
  * paths (CipherState API, batch, wire) never expose unverified plaintext
  * either way: they stage records in library memory and copy out only
  * verified ones; they set this flag (strict order) by default. */

@@ -56,7 +56,6 @@ bool uniform_fast(const NoiseAeadUniform *j, bool open)
     return true;
 }
 
-bool verify_first(const NoiseAeadUniform *j, bool open);
 
 /* One lane per record (chachapoly.hip seal_solo_staged) for uniform FAST
    batches from SOLO_MIN_RECORDS on: one Poly1305 chain per record with the
@@ -152,10 +151,18 @@ UniformArgs to_args(const NoiseAeadUniform *j)
     return a;
 }
 
-bool verify_first(const NoiseAeadUniform *j, bool open)
+/* The open order of a job: verify first under NOISE_AEAD_FLAG_VERIFY_FIRST,
+   and always for AES-GCM — there it costs nothing (C3 732 vs 726 GiB/s, the
+   C5 AES-GCM open 0.77 vs 0.82 ms: the GHASH-only pass, then CTR for the
+   verified records, profiles/r04_round/), so AES-GCM opens have the
+   reference's order (cipher-aesgcm.c:172-188) on every path.  ChaChaPoly
+   keeps the one-pass order by default (verify-first costs 15-20 %,
+   DESIGN.md 4.1b). */
+bool open_vf(int cipher_id, uint32_t flags, bool open)
 {
-    return open && (j->flags & NOISE_AEAD_FLAG_VERIFY_FIRST);
+    return open && ((flags & NOISE_AEAD_FLAG_VERIFY_FIRST) || cipher_id == NOISE_CIPHER_AESGCM);
 }
+
 
 /* NOISE_AEAD_FLAG_CT_GHASH, or NOISE_AEAD_CT_GHASH=1 in the environment
    (read once) for every job */
@@ -174,7 +181,7 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     if (rc) return rc;
     hipStream_t s = (hipStream_t)stream;
     UniformArgs a = to_args(job);
-    a.vf = verify_first(job, open);
+    a.vf = open_vf(cipher_id, job->flags, open);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         const int k = uniform_lanes(job, open);
         const bool ukey = (k >= 4 || k == 1) && job->recs_per_state % (64u / (uint32_t)k) == 0;
@@ -270,7 +277,7 @@ int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform
     /* a VERIFY_FIRST open shares a launch only with kernels that run its
        order: the one-lane ChaChaPoly open (AUTH + DEC passes) and the staged
        AES-GCM open (GHASH, verdict, then CTR) */
-    const bool vf = verify_first(oj, true);
+    const bool vf = open_vf(cipher_id, oj->flags, true);
     UniformArgs oa = to_args(oj);
     oa.vf = vf;
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY && sj->n_records && oj->n_records) {
@@ -309,7 +316,7 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
     a.ad = job->ad;
     a.status = job->status;
     a.n_records = job->n_records;
-    a.vf = open && (job->flags & NOISE_AEAD_FLAG_VERIFY_FIRST);
+    a.vf = open_vf(cipher_id, job->flags, open);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         int k = job->lanes_per_record ? (int)job->lanes_per_record : auto_lanes(job->n_records, 0);
         /* ragged records are often long (C5 mixes 64 B-16 KiB): 8 lanes up to

@@ -224,6 +224,8 @@ def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     good = torch.ones(N, dtype=torch.bool, device="cuda")
     good[torch.from_numpy(bad).to("cuda")] = False
     assert torch.equal(bv[good], pv[good])
-    # rejected records: zeroed out of place (one pass) / never written (verify-first)
-    assert int(bv[~good].max().item()) == (0xA5 if vf else 0)
-    assert int(bv[~good].min().item()) == (0xA5 if vf else 0)
+    # rejected records: zeroed out of place (one-pass ChaChaPoly) / never
+    # written (verify-first, and every AES-GCM open)
+    fill = 0xA5 if (vf or cipher == A.AESGCM) else 0
+    assert int(bv[~good].max().item()) == fill
+    assert int(bv[~good].min().item()) == fill
