@@ -171,6 +171,35 @@ NA_DEV void chacha_quad(const uint32_t key[8], uint32_t ctr, uint32_t n_lo, uint
     oa = a + a0; ob = b + b0; oc = cc + c0; od = d + d0;
 }
 
+/* chacha_quad for two blocks at once (blocks ctr0 and ctr1 on the same
+   quad): two independent dependency chains in one instruction stream, so a
+   lone wave's issue slots fill with the other block's work (the multi-pass
+   records' passes, two per step) */
+NA_DEV void chacha_quad_x2(const uint32_t key[8], uint32_t ctr0, uint32_t ctr1, uint32_t n_lo, uint32_t n_hi,
+                           int c, uint32_t o0[4], uint32_t o1[4])
+{
+    const uint32_t a0 = c == 0 ? 0x61707865u : c == 1 ? 0x3320646eu : c == 2 ? 0x79622d32u : 0x6b206574u;
+    const uint32_t b0 = c == 0 ? key[0] : c == 1 ? key[1] : c == 2 ? key[2] : key[3];
+    const uint32_t c0 = c == 0 ? key[4] : c == 1 ? key[5] : c == 2 ? key[6] : key[7];
+    const uint32_t d0 = c == 0 ? ctr0 : c == 1 ? 0u : c == 2 ? n_lo : n_hi;
+    const uint32_t d1 = c == 0 ? ctr1 : d0;
+    uint32_t a = a0, b = b0, cc = c0, d = d0;
+    uint32_t e = a0, f = b0, g = c0, h = d1;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        NA_QR(a, b, cc, d);
+        NA_QR(e, f, g, h);
+        b = quad_perm<QP_NEXT1>(b); cc = quad_perm<QP_NEXT2>(cc); d = quad_perm<QP_NEXT3>(d);
+        f = quad_perm<QP_NEXT1>(f); g = quad_perm<QP_NEXT2>(g); h = quad_perm<QP_NEXT3>(h);
+        NA_QR(a, b, cc, d);
+        NA_QR(e, f, g, h);
+        b = quad_perm<QP_NEXT3>(b); cc = quad_perm<QP_NEXT2>(cc); d = quad_perm<QP_NEXT1>(d);
+        f = quad_perm<QP_NEXT3>(f); g = quad_perm<QP_NEXT2>(g); h = quad_perm<QP_NEXT1>(h);
+    }
+    o0[0] = a + a0; o0[1] = b + b0; o0[2] = cc + c0; o0[3] = d + d0;
+    o1[0] = e + a0; o1[1] = f + b0; o1[2] = g + c0; o1[3] = h + d1;
+}
+
 /* 16 bytes at p (16-B aligned LDS), bytes from `n` on cleared */
 NA_DEV void lds_block(const uint8_t *p, uint32_t n, uint32_t w[4])
 {
@@ -334,6 +363,36 @@ NA_DEV bool worker_chacha_fast(uint8_t *rec, const uint8_t *ad, uint32_t ad_len,
    0 for r and s) and decrypts only a verified record.  A separate
    instantiation, so records of one pass keep worker_chacha_fast unchanged
    (round 3 measured a merged version costing them 0.3-0.8 us). */
+/* XOR the key stream of blocks 1..J into the record in LDS: pass p holds
+   blocks 64p + q (pass 0's key stream, ks0, computed already); the other
+   passes two at a time (chacha_quad_x2) */
+NA_DEV void multi_xor_one(uint8_t *rec, uint32_t v, uint32_t J, int c, const uint32_t ks[4])
+{
+    if (v >= 1 && v <= J) {
+        uint32_t *w = (uint32_t *)(rec + 64 * (v - 1) + 4 * c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[4 * i] ^= ks[i];
+    }
+}
+
+NA_DEV void multi_xor_passes(uint8_t *rec, const uint32_t key[8], uint32_t n_lo, uint32_t n_hi, int c, uint32_t q,
+                             uint32_t J, uint32_t P, const uint32_t ks0[4])
+{
+    multi_xor_one(rec, q, J, c, ks0);
+    for (uint32_t p = 1; p < P; p += 2) {
+        const uint32_t v0 = 64 * p + q, v1 = v0 + 64;
+        uint32_t k0[4], k1[4];
+        if (p + 1 < P) { /* uniform */
+            chacha_quad_x2(key, v0, v1, n_lo, n_hi, c, k0, k1);
+            multi_xor_one(rec, v0, J, c, k0);
+            multi_xor_one(rec, v1, J, c, k1);
+        } else {
+            chacha_quad(key, v0, n_lo, n_hi, c, k0[0], k0[1], k0[2], k0[3]);
+            multi_xor_one(rec, v0, J, c, k0);
+        }
+    }
+}
+
 template <bool OPEN>
 NA_DEV bool worker_chacha_multi(uint8_t *rec, const uint8_t *ad, uint32_t ad_len, uint32_t len,
                                 const uint8_t *key8, uint64_t nonce, FastLds &F)
@@ -350,22 +409,7 @@ NA_DEV bool worker_chacha_multi(uint8_t *rec, const uint8_t *ad, uint32_t ad_len
     uint32_t ks0[4] = {0, 0, 0, 0}; /* pass 0 (open: XORed after the verdict) */
     chacha_quad(key, q, n_lo, n_hi, c, ks0[0], ks0[1], ks0[2], ks0[3]);
     if (q == 0) { F.rs[c] = ks0[0]; F.rs[4 + c] = ks0[1]; }
-    if (!OPEN) {
-        for (uint32_t p = 0; p < P; ++p) {
-            const uint32_t v = 64 * p + q;
-            uint32_t ks[4];
-            if (p == 0) {
-                ks[0] = ks0[0]; ks[1] = ks0[1]; ks[2] = ks0[2]; ks[3] = ks0[3];
-            } else if (v <= J) {
-                chacha_quad(key, v, n_lo, n_hi, c, ks[0], ks[1], ks[2], ks[3]);
-            }
-            if (v >= 1 && v <= J) {
-                uint32_t *w = (uint32_t *)(rec + 64 * (v - 1) + 4 * c);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) w[4 * i] ^= ks[i]; /* CT; bytes past len: the tag overwrites */
-            }
-        }
-    }
+    if (!OPEN) multi_xor_passes(rec, key, n_lo, n_hi, c, q, J, P, ks0); /* CT; bytes past len: the tag overwrites */
     __syncthreads();
     NA_FSTAMP(0); /* seal: CT in LDS; both: r and s published */
     const uint32_t a = (ad_len + 15) / 16, m = (len + 15) / 16, n = a + m + 1;
@@ -431,22 +475,7 @@ NA_DEV bool worker_chacha_multi(uint8_t *rec, const uint8_t *ad, uint32_t ad_len
     if (!OPEN) return true;
     __syncthreads();
     const bool ok = F.verdict != 0;
-    if (ok) { /* decrypt the verified record in LDS */
-        for (uint32_t p = 0; p < P; ++p) {
-            const uint32_t v = 64 * p + q;
-            uint32_t ks[4];
-            if (p == 0) {
-                ks[0] = ks0[0]; ks[1] = ks0[1]; ks[2] = ks0[2]; ks[3] = ks0[3];
-            } else if (v <= J) {
-                chacha_quad(key, v, n_lo, n_hi, c, ks[0], ks[1], ks[2], ks[3]);
-            }
-            if (v >= 1 && v <= J) {
-                uint32_t *w = (uint32_t *)(rec + 64 * (v - 1) + 4 * c);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) w[4 * i] ^= ks[i]; /* bytes past len: not copied out */
-            }
-        }
-    }
+    if (ok) multi_xor_passes(rec, key, n_lo, n_hi, c, q, J, P, ks0); /* decrypt the verified record in LDS */
     NA_FSTAMP(4);
 #undef NA_FSTAMP
     return ok;
