@@ -1164,6 +1164,10 @@ NA_DEV void dma16_asm(const void *g, uint32_t lds)
    about to be read, issued a step earlier, and the stores issued with it) */
 NA_DEV void solo_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+/* all but the youngest 8 (one step's DMA) done: the AUTH pass keeps two
+   steps in flight */
+NA_DEV void solo_wait_step_old() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+
 /* DMA of step m (units 2m, 2m+1) of the wave's records into tile t.  Chunks
    at or past lim (= 64 J, the end of the record's last unit) re-read the
    step's first unit instead: FAST slots are only readable up to
@@ -1269,24 +1273,24 @@ NA_DEV SoloRec solo_rec(const UniformArgs &a, uint32_t wave_job)
    after issuing the next DMA, as the 4-lane kernels do, made every step wait
    for the DMA it had just issued and serialised the stores behind it.) */
 /* solo_pass modes: SEAL and OPEN1 (one-pass open) as above; the
-   verify-first open runs AUTH (Poly1305 over the CT, nothing written) and
-   then DEC over the verified records (key stream only; stores gated by
-   okm, the owners' verdicts per coalesced instruction, and ok). */
-enum SoloMode { SOLO_SEAL, SOLO_OPEN1, SOLO_AUTH, SOLO_DEC };
+   verify-first open runs solo_auth (below) and then DEC over the verified
+   records (key stream only; stores gated by okm, the owners' verdicts per
+   coalesced instruction, and ok). */
+enum SoloMode { SOLO_SEAL, SOLO_OPEN1, SOLO_DEC };
 
 template <int MODE>
 NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const uint32_t key[8],
                       const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, const R32 &r, P32 &h,
                       uint32_t okm = 0xffu, bool ok = true)
 {
-    constexpr bool STORES = MODE != SOLO_AUTH, KEYSTREAM = MODE != SOLO_AUTH, POLY = MODE != SOLO_DEC;
+    constexpr bool POLY = MODE != SOLO_DEC;
     for (uint32_t m = 0; m < q.S; ++m) {
         uint4 *cur = tiles + SOLO_TILE * (m & 1), *nxt = tiles + SOLO_TILE * ((m + 1) & 1);
         uint32_t wu[2][16];
         solo_wait();
         solo_get(cur, q.lane, 0, wu[0]);
         solo_get(cur, q.lane, 1, wu[1]);
-        if (STORES && m >= 1) solo_store(a, q.rec0, q.lane, m - 1, q.full_lim, nxt, okm);
+        if (m >= 1) solo_store(a, q.rec0, q.lane, m - 1, q.full_lim, nxt, okm);
         __builtin_amdgcn_wave_barrier();
         if (m + 1 < q.S) solo_dma(a, q.rec0, q.lane, m + 1, q.lim, nxt);
         /* Two waves share a SIMD and the older one takes the issue slots:
@@ -1294,29 +1298,25 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
            second finished alone, at one wave's issue rate.  A wave that is
            ahead lowers its priority (aead_device.h): C2 +5-8 %, C4 +0.5 %
            (profiles/r04/solo_prio_ab.jsonl). */
-        if (KEYSTREAM) prio_by_progress(m, q.S);
+        prio_by_progress(m, q.S);
 #ifdef NA_SOLO_X2
         uint32_t xs[2][16];
-        if (KEYSTREAM) {
-            if (2 * m + 1 < q.J) chacha20_2block_pre(key, pre, 2 * m + 1, 2 * m + 2, n_lo, n_hi, xs[0], xs[1]);
-            else chacha20_block_pre(key, pre, 2 * m + 1, n_lo, n_hi, xs[0]);
-        }
+        if (2 * m + 1 < q.J) chacha20_2block_pre(key, pre, 2 * m + 1, 2 * m + 2, n_lo, n_hi, xs[0], xs[1]);
+        else chacha20_block_pre(key, pre, 2 * m + 1, n_lo, n_hi, xs[0]);
 #endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u; /* unit, ChaCha block j + 1 */
             if (j < q.J) {
                 uint32_t x[16], w[16];
-                if constexpr (KEYSTREAM) {
 #ifdef NA_SOLO_X2
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
+                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
 #else
-                    chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+                chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
 #endif
-                }
                 uint32_t nb = 4;
-                if constexpr (MODE == SOLO_OPEN1 || MODE == SOLO_AUTH) {
+                if constexpr (MODE == SOLO_OPEN1) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) w[i] = wu[u][i];
                     if (j == q.J - 1) { /* bytes past len are never stored */
@@ -1324,11 +1324,9 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
                         nb = (q.tail + 15) / 16;
                     }
                     p32_unit(h, r, w, nb);
-                    if constexpr (MODE == SOLO_OPEN1) {
 #pragma unroll
-                        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-                        if (j == q.J - 1 && q.live) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
-                    }
+                    for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+                    if (j == q.J - 1 && q.live) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
                 } else {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) w[i] = wu[u][i] ^ x[i];
@@ -1341,11 +1339,11 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
                     }
                     if constexpr (POLY) p32_unit(h, r, w, nb);
                 }
-                if constexpr (STORES) solo_put(cur, q.lane, u, w);
+                solo_put(cur, q.lane, u, w);
             }
         }
     }
-    if (STORES && q.S) {
+    if (q.S) {
         __builtin_amdgcn_wave_barrier();
         solo_store(a, q.rec0, q.lane, q.S - 1, q.full_lim, tiles + SOLO_TILE * ((q.S - 1) & 1), okm);
     }
@@ -1368,6 +1366,45 @@ NA_DEV void seal_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
     uint32_t tag[4];
     solo_tag(h, r, a.ad_len, q.len, s, tag);
     if (q.live) tag_out(u_dst(a, q.rc) + q.len, q.len, tag);
+}
+
+/* The verify-first open's AUTH pass: Poly1305 over the ciphertext only,
+   nothing stored, so both tiles serve as a two-deep queue — a step's units
+   are read into registers and the tile takes the DMA two steps ahead
+   (DMA(0) was issued by the caller).  At top priority: it takes the issue
+   slots it needs as its loads land while the SIMD's other wave computes
+   (tools/microbench/timeline_solo.hip, steady state: 133 -> 125 us per C2
+   duplex launch; at the default priority the seal wave beside it starved
+   it). */
+NA_DEV void solo_auth(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const R32 &r, P32 &h)
+{
+    if (q.S > 1) solo_dma(a, q.rec0, q.lane, 1, q.lim, tiles + SOLO_TILE);
+    for (uint32_t m = 0; m < q.S; ++m) {
+        uint4 *cur = tiles + SOLO_TILE * (m & 1);
+        uint32_t wu[2][16];
+        if (m + 1 < q.S) solo_wait_step_old();
+        else solo_wait();
+        solo_get(cur, q.lane, 0, wu[0]);
+        solo_get(cur, q.lane, 1, wu[1]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the tile is read before the DMA refills it */
+        __builtin_amdgcn_wave_barrier();
+        if (m + 2 < q.S) solo_dma(a, q.rec0, q.lane, m + 2, q.lim, cur);
+#ifndef NA_SOLO_NO_AUTH_PRIO
+        __builtin_amdgcn_s_setprio(3);
+#endif
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t j = 2 * m + u;
+            if (j < q.J) {
+                uint32_t nb = 4;
+                if (j == q.J - 1) {
+                    mask_unit(wu[u], q.tail);
+                    nb = (q.tail + 15) / 16;
+                }
+                p32_unit(h, r, wu[u], nb);
+            }
+        }
+    }
 }
 
 /* Open, one pass: Poly1305 over each ciphertext unit as it arrives, then
@@ -1394,13 +1431,17 @@ NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
     uint32_t s[4];
     P32 h;
     solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, rc) : nullptr, a.ad_len, r, s, h);
-    if (a.vf) solo_pass<SOLO_AUTH>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
+    if (a.vf) solo_auth(a, q, tiles, r, h);
     else solo_pass<SOLO_OPEN1>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
     uint32_t tag[4], got[4];
     solo_tag(h, r, a.ad_len, len, s, tag);
     tag_in<true>(u_src(a, rc), len, got); /* the tag bytes are never written */
     const bool ok = tag_equal(tag, got);
     if (live && a.status) a.status[rec_raw] = ok ? 0 : 1;
+#ifndef NA_SOLO_AUTH_HOOK
+#define NA_SOLO_AUTH_HOOK() /* tools/microbench/timeline_solo.hip stamps the AUTH pass's end here */
+#endif
+    NA_SOLO_AUTH_HOOK();
     if (a.vf) {
         if (__ballot(live && ok) == 0) return;
         uint32_t okm = 0; /* bit i: the owner coalesced instruction i serves verified */
