@@ -199,7 +199,7 @@ int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_
  *           unauthenticated plaintext, which the kernel undoes (restores /
  *           zeroes) before it completes.  With NOISE_AEAD_FLAG_VERIFY_FIRST
  *           they take the reference's order (cipher-chachapoly.c:135-141),
- *           as AESGCM does, at 15-20 % of the batch rate.
+ *           as AESGCM does, at about 12 % of the batch rate.
  * Memory: input and output records must be either exactly in place
  * (in == out and in_stride == out_stride) or disjoint record by record:
  * with one stride for both sides the records may interleave (input and

@@ -156,7 +156,7 @@ UniformArgs to_args(const NoiseAeadUniform *j)
    C5 AES-GCM open 0.77 vs 0.82 ms: the GHASH-only pass, then CTR for the
    verified records, profiles/r04_round/), so AES-GCM opens have the
    reference's order (cipher-aesgcm.c:172-188) on every path.  ChaChaPoly
-   keeps the one-pass order by default (verify-first costs 15-20 %,
+   keeps the one-pass order by default (verify-first costs about 12 %,
    DESIGN.md 4.1b). */
 bool open_vf(int cipher_id, uint32_t flags, bool open)
 {
