@@ -644,7 +644,6 @@ class UniformWork:
             st = torch.full((N,), 0xFF, dtype=torch.uint8, device=dev)
             self.sets.append((pt, ct, back, st))
         torch.cuda.synchronize(dev)
-        self.lanes = args.lanes or A.dev_default_lanes(cipher, N)
         self.sflags = A.FLAG_CT_GHASH if args.ct_ghash else 0
         self.oflags = self.sflags | (A.FLAG_VERIFY_FIRST if args.verify_first else 0)
         # Each step seals set b = s % sets and opens set (s - LAG) % sets, sealed
@@ -654,6 +653,12 @@ class UniformWork:
         # every open has ciphertext; a set's ciphertext is the same at every seal.
         self.lag = 2 if args.sets >= 3 else 0
         self.duplex = args.mode == "duplex"
+        # lanes 0 in the jobs: the library's own choice, which differs
+        # between a duplex launch and standalone seals/opens; self.lanes is
+        # the duplex (timed) launch's, for the kernel names
+        self.job_lanes = args.lanes
+        self.lanes = args.lanes or (A.dev_duplex_lanes(cipher, N) if self.duplex else
+                                    A.dev_default_lanes(cipher, N))
         self.per_step = args.events == "step"
         # --streams 2 (separate mode): consecutive steps (independent batch
         # sets) alternate between two streams, so step s+1's seal can start on
@@ -668,7 +673,7 @@ class UniformWork:
 
     def _common(self):
         return dict(ctx=self.ctx.data_ptr(), nonce_base=self.nonce.data_ptr(), length=self.L,
-                    n_records=self.N, recs_per_state=self.sh["rps"], lanes=self.lanes, **self.ad_kw)
+                    n_records=self.N, recs_per_state=self.sh["rps"], lanes=self.job_lanes, **self.ad_kw)
 
     def seal(self, b, pt=None, ct=None, stream=None):
         if pt is None:

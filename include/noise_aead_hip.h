@@ -413,12 +413,18 @@ void *noise_aead_debug_last_freed_ctx(size_t *bytes);
  *   current device whose kernel is still running (-1: no device). */
 int noise_aead_debug_workers_resident(void);
 
-/* Default lanes per record the library picks for a uniform batch of n
- * records in a FAST layout (16-B aligned slots readable up to roundup64(len)):
- * ChaChaPoly 1 from 64 Ki records on (one lane per record, LDS-staged), else
- * 4 or 8, and up to 64 for batches of at most 512 records; AES-GCM 4.  Other
- * layouts, VERIFY_FIRST opens and ragged batches keep the multi-lane rule. */
+/* Default lanes per record the library picks for a standalone uniform seal
+ * or open of n records (noise_aead_dev_{seal,open}_uniform, lanes 0) in a
+ * FAST layout: ChaChaPoly 1 from 128 Ki records (the one-lane kernels at
+ * two waves per SIMD), else 4 or 8, and up to 64 for batches of at most 512
+ * records (a VERIFY_FIRST open of at least 64 Ki records: 1); AES-GCM 4.
+ * Other layouts and ragged batches keep the multi-lane rules. */
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records);
+/* ...and for each job of a noise_aead_dev_duplex_uniform launch: ChaChaPoly
+ * jobs of at least 64 Ki records in FAST layouts (16-B aligned slots
+ * readable up to roundup64(len)) take one lane per record (the LDS-staged
+ * one-lane kernels, a seal and an open wave on every SIMD), else as above. */
+int noise_aead_dev_duplex_lanes(int cipher_id, uint32_t n_records);
 
 /* Deterministic synthetic bytes (bench/test input): 64-bit LE word w of the
  * output = SplitMix64(seed + word0 + w), SURVEY.md §8d. */

@@ -57,13 +57,20 @@ bool uniform_fast(const NoiseAeadUniform *j, bool open)
 }
 
 
-/* One lane per record (chachapoly.hip seal_solo_staged) for uniform FAST
-   batches from SOLO_MIN_RECORDS on: one Poly1305 chain per record with the
-   clamped r, the per-record work paid once per 64 records; C2 +8-9 %, C4
-   +13 % over four lanes (profiles/r04/solo_ab.jsonl).  Below that the
-   batch is under one wave per SIMD at one lane.  NOISE_AEAD_SOLO=0 keeps
-   the 4-lane kernels (A/B runs). */
+/* One lane per record (chachapoly.hip seal_solo_staged) for the duplex
+   launch of two uniform FAST jobs of at least SOLO_MIN_RECORDS each: one
+   Poly1305 chain per record with the clamped r, the per-record work paid
+   once per 64 records, and a seal and an open wave on every SIMD; C2
+   +8-17 %, C4 +13-18 % over four lanes (profiles/r04/solo_ab.jsonl,
+   solo_prio_ab.jsonl).  A standalone seal or open takes one lane from
+   SOLO_MIN_STANDALONE records, two waves per SIMD: C4's 1 Mi records as
+   back-to-back seal and open launches 1624-1636 vs 1410-1415 GiB/s at four
+   lanes, while a 64 Ki-record job alone (one wave per SIMD) runs 3 % faster
+   at four lanes (1315-1321 vs 1280-1283, profiles/r04/separate_lanes_ab.jsonl)
+   — except a VERIFY_FIRST open, which the 4/8-lane staged kernels do not
+   run.  NOISE_AEAD_SOLO=0 keeps the 4-lane kernels everywhere (A/B runs). */
 constexpr uint32_t SOLO_MIN_RECORDS = 65536;
+constexpr uint32_t SOLO_MIN_STANDALONE = 2 * SOLO_MIN_RECORDS;
 
 bool solo_enabled()
 {
@@ -74,10 +81,12 @@ bool solo_enabled()
     return on;
 }
 
-int uniform_lanes(const NoiseAeadUniform *j, bool open)
+int uniform_lanes(const NoiseAeadUniform *j, bool open, bool duplex)
 {
     if (j->lanes_per_record) return (int)j->lanes_per_record;
-    if (j->n_records >= SOLO_MIN_RECORDS && solo_enabled() && uniform_fast(j, open)) return 1;
+    if (j->n_records >= SOLO_MIN_RECORDS && solo_enabled() && uniform_fast(j, open) &&
+        (duplex || j->n_records >= SOLO_MIN_STANDALONE || (open && (j->flags & NOISE_AEAD_FLAG_VERIFY_FIRST))))
+        return 1;
     return auto_lanes(j->n_records, 0);
 }
 
@@ -183,7 +192,7 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     UniformArgs a = to_args(job);
     a.vf = open_vf(cipher_id, job->flags, open);
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
-        const int k = uniform_lanes(job, open);
+        const int k = uniform_lanes(job, open, false);
         const bool ukey = (k >= 4 || k == 1) && job->recs_per_state % (64u / (uint32_t)k) == 0;
         /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC): open
            balances its waves' progress (profiles/r01_prio_ab.jsonl); in the
@@ -281,7 +290,7 @@ int run_duplex(int cipher_id, const NoiseAeadUniform *sj, const NoiseAeadUniform
     UniformArgs oa = to_args(oj);
     oa.vf = vf;
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY && sj->n_records && oj->n_records) {
-        const int ks = uniform_lanes(sj, false), ko = uniform_lanes(oj, true);
+        const int ks = uniform_lanes(sj, false, true), ko = uniform_lanes(oj, true, true);
         const bool us = (ks >= 4 || ks == 1) && sj->recs_per_state % (64u / (uint32_t)ks) == 0;
         const bool uo = (ko >= 4 || ko == 1) && oj->recs_per_state % (64u / (uint32_t)ko) == 0;
         if (ks == ko && (ks == 1 || ((ks == 4 || ks == 8) && !vf)) && us == uo && uniform_fast(sj, false) &&
@@ -552,9 +561,15 @@ int noise_aead_dev_pad(NoiseRandSnapshot *d_rand, uint8_t *d_payloads, uint64_t 
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)
 {
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY)
-        return n_records >= SOLO_MIN_RECORDS && solo_enabled() ? 1 : auto_lanes(n_records, 0);
+        return n_records >= SOLO_MIN_STANDALONE && solo_enabled() ? 1 : auto_lanes(n_records, 0);
     if (cipher_id == NOISE_CIPHER_AESGCM) return GCM_LANES;
     return 0;
+}
+
+int noise_aead_dev_duplex_lanes(int cipher_id, uint32_t n_records)
+{
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY && n_records >= SOLO_MIN_RECORDS && solo_enabled()) return 1;
+    return noise_aead_dev_default_lanes(cipher_id, n_records);
 }
 
 /* NOISE_AEAD_LANES=narrow: the host paths keep K <= 8 and the 4-lane AES

@@ -143,6 +143,7 @@ def lib() -> C.CDLL:
         "noise_aead_dev_seal_ragged": (i, [i, P(NoiseAeadRagged), vp]),
         "noise_aead_dev_open_ragged": (i, [i, P(NoiseAeadRagged), vp]),
         "noise_aead_dev_default_lanes": (i, [i, C.c_uint32]),
+        "noise_aead_dev_duplex_lanes": (i, [i, C.c_uint32]),
         "noise_aead_dev_pad": (i, [vp, vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, i, vp, vp]),
         "noise_strerror": (i, [i, C.c_char_p, sz]),
         "noise_perror": (None, [C.c_char_p, i]),
@@ -425,3 +426,7 @@ def dev_fill_splitmix(d_out: int, nbytes: int, seed: int, word0: int = 0, stream
 
 def dev_default_lanes(cipher: int, n_records: int) -> int:
     return lib().noise_aead_dev_default_lanes(cipher, n_records)
+
+
+def dev_duplex_lanes(cipher: int, n_records: int) -> int:
+    return lib().noise_aead_dev_duplex_lanes(cipher, n_records)

@@ -182,15 +182,20 @@ def test_batch_host_rules(aead_built):
 
 def test_default_lane_policy(aead_built):
     """Lanes per record the library picks (aead_api.hip uniform_lanes /
-    auto_lanes): one lane per record at the BASELINE sizes (64 Ki records and
-    up, FAST layouts), 8 below 64 Ki records, and wide groups (up to a wave per
-    record) only for batches of at most 512 records — the latency regime."""
+    auto_lanes): a standalone seal or open takes one lane per record from
+    128 Ki records (two waves per SIMD), 4 lanes from 64 Ki, 8 below, and wide
+    groups (up to a wave per record) only for batches of at most 512 records
+    — the latency regime; the jobs of a duplex launch take one lane per
+    record from 64 Ki records (the BASELINE sizes, FAST layouts)."""
     A = aead_built
     lanes = lambda n: A.dev_default_lanes(A.CHACHAPOLY, n)
-    assert lanes(65536) == 1 and lanes(1 << 20) == 1
+    duplex = lambda n: A.dev_duplex_lanes(A.CHACHAPOLY, n)
+    assert lanes(65536) == 4 and lanes(131071) == 4 and lanes(131072) == 1 and lanes(1 << 20) == 1
     assert lanes(65535) == 8 and lanes(513) == 8
     assert lanes(512) == 64 and lanes(1) == 64
-    assert A.dev_default_lanes(A.AESGCM, 1) == 4
+    assert duplex(65536) == 1 and duplex(1 << 20) == 1
+    assert duplex(65535) == 8 and duplex(512) == 64
+    assert A.dev_default_lanes(A.AESGCM, 1) == 4 and A.dev_duplex_lanes(A.AESGCM, 1 << 20) == 4
 
 
 def test_device_api_argument_rules(aead_built):

@@ -58,7 +58,7 @@ def test_default_layout_and_kernel_names():
         n, s = c["records"], c["states"]
         ad = c.get("ad", 0)
         ins, outs = bench.stride(c["len"], 128), bench.stride(c["len"] + 16, 128)
-        lanes = A.dev_default_lanes(c["cipher"], n)  # the library's choice, as the bench takes it
+        lanes = A.dev_duplex_lanes(c["cipher"], n)  # the library's choice for the timed duplex launch
         k = bench.kernel_name(c["cipher"], n, n // s, lanes, ins, outs, c["len"], duplex=True)
         assert "_duplex_" in k, (cfg, k)
         prof = bench.load_pmc(cfg, k)
