@@ -795,7 +795,7 @@ class UniformWork:
             open_ms = sum(e[1].elapsed_time(e[2]) for e in self.ev) / steps
             return seal_ms, open_ms
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        reps, sets = 5, self.args.sets
+        reps, sets = 20, self.args.sets
         e[0].record(self.stream)
         for r in range(reps):
             self.seal(r % sets)
