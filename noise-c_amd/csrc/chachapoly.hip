@@ -1198,7 +1198,14 @@ NA_DEV void solo_store(const UniformArgs &a, uint32_t rec0, uint32_t lane, uint3
     for (int i = 0; i < 8; ++i) {
         const uint4 q = t[64 * i + lane];
         const uint32_t r = rec0 + 8u * i + (lane >> 3);
-        if (r < a.n_records && ((okm >> i) & 1)) rec_store16(a.out + (size_t)r * a.out_stride + off, q);
+        if (r < a.n_records && ((okm >> i) & 1)) {
+            /* non-temporal: the one-lane kernels' store pattern (8 x 128 B
+               per instruction) alone runs at 4.9 vs 3.8 TB/s, and C4 / perf
+               gain 1-3 % (tools/microbench/solo_dma.hip,
+               profiles/r04/nt_store_ab.jsonl) */
+            na_u32x4 v = {q.x, q.y, q.z, q.w};
+            __builtin_nontemporal_store(v, (na_u32x4 *)(a.out + (size_t)r * a.out_stride + off));
+        }
     }
 }
 
