@@ -1155,8 +1155,13 @@ NA_DEV uint32_t solo_chunk(uint32_t lane) { return (lane ^ (lane >> 3)) & 7; }
 #pragma clang diagnostic ignored "-Winline-asm"
 NA_DEV void dma16_asm(const void *g, uint32_t lds)
 {
+#ifdef NA_DMA_NT
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
+                 :: "v"(g), "s"(lds) : "memory", "m0");
+#else
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
                  :: "v"(g), "s"(lds) : "memory", "m0");
+#endif
 }
 #pragma clang diagnostic pop
 
