@@ -805,13 +805,15 @@ NA_DEV void wave_dma(const UniformArgs &a, const WaveIO<K> &io, int j0, uint4 *t
             (lds_void *)(t + 64 * i), 16, 0, 0);
 }
 
-/* A 16-B record store of the staged kernels.  NA_NT_STORE: non-temporal
-   (streaming) — the written lines need not displace the ciphertext lines
-   the next step of an open still reads from L2. */
+/* A 16-B record store of the staged kernels: non-temporal (streaming), so
+   the written lines need not displace the ciphertext lines the next step of
+   an open still reads.  Round 4: the 4-lane kernels' standalone C2 seal+open
+   +1.0-1.9 % in three interleaved rounds, C5 unchanged
+   (profiles/r04/nt_store_ab.jsonl); NA_PLAIN_STORE restores plain stores. */
 typedef uint32_t na_u32x4 __attribute__((ext_vector_type(4)));
 NA_DEV void rec_store16(uint8_t *p, const uint4 &q)
 {
-#ifdef NA_NT_STORE
+#ifndef NA_PLAIN_STORE
     na_u32x4 v = {q.x, q.y, q.z, q.w};
     __builtin_nontemporal_store(v, (na_u32x4 *)p);
 #else
@@ -1203,14 +1205,11 @@ NA_DEV void solo_store(const UniformArgs &a, uint32_t rec0, uint32_t lane, uint3
     for (int i = 0; i < 8; ++i) {
         const uint4 q = t[64 * i + lane];
         const uint32_t r = rec0 + 8u * i + (lane >> 3);
-        if (r < a.n_records && ((okm >> i) & 1)) {
-            /* non-temporal: the one-lane kernels' store pattern (8 x 128 B
-               per instruction) alone runs at 4.9 vs 3.8 TB/s, and C4 / perf
-               gain 1-3 % (tools/microbench/solo_dma.hip,
-               profiles/r04/nt_store_ab.jsonl) */
-            na_u32x4 v = {q.x, q.y, q.z, q.w};
-            __builtin_nontemporal_store(v, (na_u32x4 *)(a.out + (size_t)r * a.out_stride + off));
-        }
+        /* non-temporal (rec_store16): the one-lane kernels' store pattern
+           (8 x 128 B per instruction) alone runs at 4.9 vs 3.8 TB/s, and C4 /
+           perf gain 1-3 % (tools/microbench/solo_dma.hip,
+           profiles/r04/nt_store_ab.jsonl) */
+        if (r < a.n_records && ((okm >> i) & 1)) rec_store16(a.out + (size_t)r * a.out_stride + off, q);
     }
 }
 
