@@ -101,7 +101,7 @@ int na_worker_crypt(int cipher_id, const uint8_t *key, const void *h_ctx, uint32
     return NOISE_ERROR_NOT_APPLICABLE;
 }
 
-void na_worker_forget_ctx(void) {}
+void na_worker_forget_ctx(const void *h_ctx) { (void)h_ctx; }
 
 int noise_aead_debug_workers_resident(void) { return 0; }
 

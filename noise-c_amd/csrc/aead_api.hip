@@ -81,14 +81,43 @@ bool solo_enabled()
     return on;
 }
 
+/* Round 5: a standalone job of SOLO_MIN_RECORDS <= n < SOLO_MIN_STANDALONE
+   FAST records takes two segments per record (chachapoly_seg.hip: 2048 waves
+   at 64 Ki records, two per SIMD, each record's Poly1305 as two chains
+   joined by r^e).  NOISE_AEAD_SEG=0 keeps the four-lane staged kernels
+   there (A/B runs). */
+bool seg_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("NOISE_AEAD_SEG");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+int standalone_lanes(uint32_t n)
+{
+    if (n >= SOLO_MIN_STANDALONE) return 1;
+    return seg_enabled() ? 2 : 0;
+}
+
 int uniform_lanes(const NoiseAeadUniform *j, bool open, bool duplex)
 {
     if (j->lanes_per_record) return (int)j->lanes_per_record;
-    if (j->n_records >= SOLO_MIN_RECORDS && solo_enabled() && uniform_fast(j, open) &&
-        (duplex || j->n_records >= SOLO_MIN_STANDALONE || (open && (j->flags & NOISE_AEAD_FLAG_VERIFY_FIRST))))
-        return 1;
+    if (j->n_records >= SOLO_MIN_RECORDS && solo_enabled() && uniform_fast(j, open)) {
+        if (duplex) return 1;
+        const int k = standalone_lanes(j->n_records);
+        if (k) return k;
+        if (open && (j->flags & NOISE_AEAD_FLAG_VERIFY_FIRST)) return 1;
+    }
     return auto_lanes(j->n_records, 0);
 }
+
+/* Ragged FAST ChaChaPoly batches of at least SEG_RAGGED_MIN records with
+   automatic lanes take the segmented one-lane kernel (a per-launch plan by
+   record length, chachapoly_seg.hip); smaller ones keep the windowed 4/8-lane
+   kernels and the wide groups of the latency path. */
+constexpr uint32_t SEG_RAGGED_MIN = 16384;
 
 void job_span(const NoiseAeadUniform *j, bool out, bool open, uint64_t &lo, uint64_t &hi);
 
@@ -333,6 +362,9 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
            lengths (C5's ChaCha kernels -2.5 % seal / -4 % open at 64 Ki
            records vs 4 lanes, profiles/r02/c5_lanes_ab.jsonl) */
         if (!job->lanes_per_record && k == 4 && job->n_records < 2u * 65536u) k = 8;
+        if (!job->lanes_per_record && (job->flags & NOISE_AEAD_FLAG_FAST) && job->n_records >= SEG_RAGGED_MIN &&
+            seg_enabled())
+            return chacha_ragged_seg(a, open, s);
         return chacha_ragged(a, k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0, s);
     }
     if (cipher_id == NOISE_CIPHER_AESGCM) {
@@ -560,8 +592,11 @@ int noise_aead_dev_pad(NoiseRandSnapshot *d_rand, uint8_t *d_payloads, uint64_t 
 
 int noise_aead_dev_default_lanes(int cipher_id, uint32_t n_records)
 {
-    if (cipher_id == NOISE_CIPHER_CHACHAPOLY)
-        return n_records >= SOLO_MIN_STANDALONE && solo_enabled() ? 1 : auto_lanes(n_records, 0);
+    if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
+        if (n_records >= SOLO_MIN_RECORDS && solo_enabled() && standalone_lanes(n_records))
+            return standalone_lanes(n_records);
+        return auto_lanes(n_records, 0);
+    }
     if (cipher_id == NOISE_CIPHER_AESGCM) return GCM_LANES;
     return 0;
 }

@@ -23,7 +23,9 @@
  */
 #include "aead_device.h"
 #include "aead_kernels.h"
-#include "aes_bs.h"
+#ifdef NA_AB_KERNELS
+#include "aes_bs.h" /* the bitsliced A/B kernels only */
+#endif
 
 namespace na {
 
@@ -941,6 +943,11 @@ __global__ __launch_bounds__(GCM_WG) void gcm_duplex_fused(UniformArgs s, Unifor
     if (b < o_blocks) gcm_staged_rec<true, CT>(o, TE, L.h4[1], L.rk[1], b);
 }
 
+#ifdef NA_AB_KERNELS
+/* Built only into the A/B variant (`make -C noise-c_amd variant NAME=ab
+   DEFS=-DNA_AB_KERNELS`): the round-4 bitsliced-AES kernels, measured and
+   rejected, kept so that record can be re-run; the product
+   library does not contain them. */
 /* ---------------------- bitsliced (uniform FAST, one state per workgroup)
  *
  * Round 4 (decide AES-GCM's structure in the full kernel).  A
@@ -1222,6 +1229,8 @@ __global__ __launch_bounds__(NT) NA_BS_OCC void gcm_bs_duplex(UniformArgs s, Uni
     else gcm_bs_wg<false>(s, S, b);
 }
 #endif
+
+#endif /* NA_AB_KERNELS */
 
 /* ------------------------------ staged ragged (any mix of states / lengths)
  *

@@ -1151,21 +1151,21 @@ NA_DEV uint32_t solo_chunk(uint32_t lane) { return (lane ^ (lane >> 3)) & 7; }
    see an LDS write: it would otherwise wait for the youngest such DMA before
    every later LDS access of the wave (tile reads AND writes), i.e. for the
    next step's DMA right after issuing it.  The one-lane kernels place their
-   own s_waitcnt vmcnt(0) instead (solo_wait).  m0 carries the LDS address; no
-   other code of these kernels keeps a value in m0 across the asm. */
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
+   own s_waitcnt vmcnt(0) instead (solo_wait).  m0 carries the LDS address:
+   m0 is reserved to the compiler (a clobber of it is not honoured), so the
+   statement saves and restores it (cdna_hip_programming.md, LDS-DMA
+   recipe) — the segmented kernels fault without that. */
 NA_DEV void dma16_asm(const void *g, uint32_t lds)
 {
+    uint32_t keep;
 #ifdef NA_DMA_NT
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt"
-                 :: "v"(g), "s"(lds) : "memory", "m0");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
 #else
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-                 :: "v"(g), "s"(lds) : "memory", "m0");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
 #endif
 }
-#pragma clang diagnostic pop
 
 /* every vector-memory operation of the wave done (the DMA into the tile
    about to be read, issued a step earlier, and the stores issued with it) */
@@ -1310,22 +1310,12 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
            ahead lowers its priority (aead_device.h): C2 +5-8 %, C4 +0.5 %
            (profiles/r04/solo_prio_ab.jsonl). */
         prio_by_progress(m, q.S);
-#ifdef NA_SOLO_X2
-        uint32_t xs[2][16];
-        if (2 * m + 1 < q.J) chacha20_2block_pre(key, pre, 2 * m + 1, 2 * m + 2, n_lo, n_hi, xs[0], xs[1]);
-        else chacha20_block_pre(key, pre, 2 * m + 1, n_lo, n_hi, xs[0]);
-#endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u; /* unit, ChaCha block j + 1 */
             if (j < q.J) {
                 uint32_t x[16], w[16];
-#ifdef NA_SOLO_X2
-#pragma unroll
-                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
-#else
                 chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
-#endif
                 uint32_t nb = 4;
                 if constexpr (MODE == SOLO_OPEN1) {
 #pragma unroll
@@ -1789,6 +1779,7 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_staged(
     else seal_il_staged<K, UKEY>(s, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], wave_of(b));
 }
 
+#ifdef NA_AB_KERNELS /* measured slower (profiles/r03/persist_ab); A/B variant builds only */
 /* Persistent duplex: the same two jobs as chachapoly_duplex_staged, but a grid
    of at most the resident workgroups (4 per CU) whose waves take wave-jobs
    (64/K records of one job) from a ticket counter until none are left:
@@ -1836,6 +1827,8 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_persist(
         }
     }
 }
+
+#endif
 
 /* One lane per record (seal_solo_staged): two waves per SIMD, 16 KB of LDS
    each; 256 records per workgroup. */

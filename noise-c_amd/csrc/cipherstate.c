@@ -148,7 +148,7 @@ void *noise_aead_debug_last_freed_ctx(size_t *bytes)
 static void release_ctx(HipCipherState *st)
 {
     if (st->h_ctx) { /* the worker's pinned copy holds key material too */
-        na_worker_forget_ctx(); /* and so may a worker's LDS cache of it */
+        na_worker_forget_ctx(st->h_ctx); /* and so may a worker's LDS cache of it */
         na_clean(st->h_ctx, noise_aead_dev_ctx_bytes(st->parent.cipher_id));
         (void)hipHostFree(st->h_ctx);
         st->h_ctx = NULL;

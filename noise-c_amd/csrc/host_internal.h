@@ -85,7 +85,7 @@ NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, const void *h_c
                               size_t len, int open);
 /* a state's AES-GCM host context is being freed: workers that may cache it
    in LDS leave (and scrub it) */
-NA_HIDDEN void na_worker_forget_ctx(void);
+NA_HIDDEN void na_worker_forget_ctx(const void *h_ctx);
 
 NA_HIDDEN Staging *na_stage_get(size_t bytes);
 NA_HIDDEN int na_ensure_ctx(HipCipherState *st, Staging *sg);

@@ -27,6 +27,9 @@ NA_HIDDEN int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, 
 /* one launch sealing job a and opening job b (k = 4 or 8, FAST layouts) */
 NA_HIDDEN int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, hipStream_t s);
 NA_HIDDEN int chacha_ragged(const RaggedArgs &a, int k, bool open, bool fast, hipStream_t s);
+/* FAST ragged batch through the segmented one-lane kernel (per-launch plan,
+   chachapoly_seg.hip) */
+NA_HIDDEN int chacha_ragged_seg(const RaggedArgs &a, bool open, hipStream_t s);
 
 /* ---- launch_aes.hip */
 /* S-box / T-table of the current device, built once (private stream) */

@@ -6,6 +6,7 @@
  */
 #include "launch.h"
 #include "chachapoly.hip"
+#include "chachapoly_seg.hip"
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -93,6 +94,19 @@ KernelFn<RaggedArgs> chacha_ragged_fn(int k, bool open, bool fast, bool vf)
     return vf ? chacha_ragged_fn_t<true, true>(k, open) : chacha_ragged_fn_t<true, false>(k, open);
 }
 
+/* Resident workgroups of a kernel on this device (CUs x occupancy). */
+template <typename F>
+uint32_t resident_blocks(F fn)
+{
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || per < 1)
+        return 0;
+    return (uint32_t)(cus * per);
+}
+
+#ifdef NA_AB_KERNELS
 /* The ticket counter pair of chachapoly_duplex_persist for (device, stream):
    zeroed once, stream-ordered before the first launch; each launch leaves it
    zeroed for the next one on the same stream. */
@@ -113,18 +127,6 @@ uint32_t *ticket_counter(hipStream_t s)
         if (hipMemsetAsync(c, 0, 64, s) != hipSuccess) return nullptr;
     }
     return c;
-}
-
-/* Resident workgroups of a kernel on this device (CUs x occupancy). */
-template <typename F>
-uint32_t resident_blocks(F fn)
-{
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) != hipSuccess || per < 1)
-        return 0;
-    return (uint32_t)(cus * per);
 }
 
 /* NOISE_AEAD_DUPLEX=persist | plain selects the duplex kernel (A/B runs). */
@@ -153,10 +155,19 @@ int duplex_persist_launch(const UniformArgs &a, const UniformArgs &b, hipStream_
     return hip_rc(hipGetLastError());
 }
 
+#endif
+
 } // namespace
 
 int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, bool ukey, hipStream_t s)
 {
+    if (k == 2 && fast) {
+        /* two segments per record, LDS-staged (chachapoly_seg.hip) */
+        const bool uk = a.rps % 32 == 0;
+        KernelFn<UniformArgs> fn = open ? (uk ? chachapoly_seg2_uniform<true, true> : chachapoly_seg2_uniform<true, false>)
+                                        : (uk ? chachapoly_seg2_uniform<false, true> : chachapoly_seg2_uniform<false, false>);
+        return launch(fn, a.n_records, 2, a, s);
+    }
     KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, fast, ukey, a.vf != 0);
     if (!fn) return NOISE_ERROR_INVALID_PARAM;
     return launch(fn, a.n_records, k, a, s);
@@ -181,11 +192,13 @@ static uint32_t duplex_run_chunk()
 
 int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, hipStream_t s)
 {
+#ifdef NA_AB_KERNELS
     if (duplex_persist() && k != 1) {
         if (k == 4) return ukey ? duplex_persist_launch<4, true>(a, b, s) : duplex_persist_launch<4, false>(a, b, s);
         if (k == 8) return ukey ? duplex_persist_launch<8, true>(a, b, s) : duplex_persist_launch<8, false>(a, b, s);
         return NOISE_ERROR_INVALID_PARAM;
     }
+#endif
     const uint32_t sb = (uint32_t)(((uint64_t)a.n_records * k + 255) / 256);
     const uint32_t ob = (uint32_t)(((uint64_t)b.n_records * k + 255) / 256);
     if (k == 1) {
@@ -210,4 +223,70 @@ int chacha_ragged(const RaggedArgs &a, int k, bool open, bool fast, hipStream_t 
     return launch(fn, a.n_records, k, a, s);
 }
 
+/* Ragged FAST batch through the segmented one-lane kernel: the plan (count,
+   scan, place) in a stream-ordered scratch block, then the persistent
+   kernel, then the scratch is freed (stream-ordered too). */
+int chacha_ragged_seg(const RaggedArgs &a, bool open, hipStream_t s)
+{
+    if (a.n_records == 0) return NOISE_ERROR_NONE;
+    const size_t bytes = SEG_MAP_OFF + (size_t)a.n_records * SEG_KMAX * sizeof(uint32_t);
+    uint8_t *scratch = nullptr;
+    if (hipMallocAsync((void **)&scratch, bytes, s) != hipSuccess) return NOISE_ERROR_NO_MEMORY;
+    SegPlanHdr *p = (SegPlanHdr *)scratch;
+#ifdef NA_SEG_DEBUG
+    {
+        uint64_t r[2] = {(uint64_t)(uintptr_t)scratch, (uint64_t)(uintptr_t)scratch + bytes};
+        (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_seg_arena), r, sizeof(r), 2 * sizeof(uint64_t),
+                                     hipMemcpyHostToDevice, s);
+    }
+#endif
+    uint32_t *map = (uint32_t *)(scratch + SEG_MAP_OFF);
+    int rc = hip_rc(hipMemsetAsync(p, 0, sizeof(SegPlanHdr), s));
+    const uint32_t pb = (a.n_records + 1023) / 1024;
+    if (!rc) {
+        hipLaunchKernelGGL(seg_plan_count, dim3(pb), dim3(1024), 0, s, a.recs, a.n_records, p);
+        hipLaunchKernelGGL(seg_plan_scan, dim3(1), dim3(64), 0, s, p);
+        hipLaunchKernelGGL(seg_plan_place, dim3(pb), dim3(1024), 0, s, a.recs, a.n_records, p, map, a.status);
+        rc = hip_rc(hipGetLastError());
+    }
+    if (!rc) {
+        auto fn = open ? chachapoly_seg_ragged<true> : chachapoly_seg_ragged<false>;
+        static uint32_t resident[2] = {0, 0}; /* one device model per process: MI355X */
+        uint32_t &res = resident[open ? 1 : 0];
+        if (!res) res = resident_blocks(fn);
+        const uint64_t most = ((uint64_t)a.n_records * SEG_KMAX + 255) / 256; /* jobs / 4, at most */
+        const uint32_t grid = (uint32_t)(res && most > res ? res : (most ? most : 1));
+        if (!res) rc = NOISE_ERROR_SYSTEM;
+        else {
+            worker_park_for_batch(grid);
+            hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, s, a, p, (const uint32_t *)map);
+            rc = hip_rc(hipGetLastError());
+        }
+    }
+    (void)hipFreeAsync(scratch, s);
+    return rc;
+}
+
 } // namespace na
+
+#ifdef NA_SEG_DEBUG
+/* debug variant only: the caller's buffer range the segmented kernels may
+   touch, and the accesses they skipped (address, kind << 56 | n << 40 | info) */
+extern "C" int noise_aead_debug_seg_arena(uint64_t lo, uint64_t hi)
+{
+    uint64_t r[2] = {lo, hi};
+    uint32_t z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(na::g_seg_arena), r, sizeof(r), 0, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(na::g_seg_nviol), &z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+
+extern "C" int noise_aead_debug_seg_viol(uint64_t *out, int n)
+{
+    uint32_t cnt = 0;
+    if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(na::g_seg_nviol), sizeof(cnt), 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (n > 64) n = 64;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(na::g_seg_viol), sizeof(uint64_t) * n, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return (int)cnt;
+}
+#endif

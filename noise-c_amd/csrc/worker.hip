@@ -102,7 +102,11 @@ struct alignas(128) WorkerSlot {
     uint32_t c1[4];    /* seq, nonce lo, nonce hi, cipher */
     uint32_t c2[4];    /* seq, ctx lo, ctx hi, stop */
     uint32_t c3[4];    /* seq, ctx generation, 0, 0 */
-    uint8_t pad0[128 - 64];
+    /* stop (word 0): its own chunk, written only by park / stop / launch —
+       never by a request's header (a header written after a
+       park used to carry stop = 0 and cancel it) */
+    uint32_t c4[4];
+    uint8_t pad0[128 - 80];
     /* worker -> host */
     uint64_t done;     /* last request completed */
     uint32_t status;   /* 0 ok, 1 MAC failure, 2 input never arrived */
@@ -560,8 +564,8 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
            request then re-reads its chunks once (stamp 0 is never current).
            A wave may see the previous poll's setting: both are correct. */
         uint4 c = make_uint4(0, 0, 0, 0), mine = make_uint4(0, 0, 0, 0);
-        if (!s_slow) load_sys16x2(req + 4 * (t & (vram ? 7 : 3)), (const uint32_t *)(in + t), c, mine);
-        else if (t < 64) c = load_sys16(req + 4 * (t & (vram ? 7 : 3)));
+        if (!s_slow) load_sys16x2(req + 4 * (t & (vram ? 15 : 7)), (const uint32_t *)(in + t), c, mine);
+        else if (t < 64) c = load_sys16(req + 4 * (t & (vram ? 15 : 7)));
         if (t == 0) s_stale = 0;
         if (t < 64) {
             const uint32_t s0 = __shfl((int)c.x, 0, 64);
@@ -570,13 +574,13 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
             if (!vram) { /* chunk k = {seq, A_k, B_k, C_k} */
                 const uint32_t s1 = __shfl((int)c.x, 1, 64);
                 const uint32_t s2 = __shfl((int)c.x, 2, 64), s3 = __shfl((int)c.x, 3, 64);
-                stop = __shfl((int)c.w, 2, 64);
+                stop = __shfl((int)c.x, 4, 64); /* chunk 4: the stop word */
                 fresh = s0 != last && s0 == s1 && s0 == s2 && s0 == s3;
                 if (t < 4) {
                     hdr[4 * t] = c.x; hdr[4 * t + 1] = c.y; hdr[4 * t + 2] = c.z; hdr[4 * t + 3] = c.w;
                 }
             } else { /* chunk 2k = {seq, A_k, seq, B_k}, 2k + 1 = {seq, C_k, seq, 0} */
-                stop = __shfl((int)c.y, 5, 64);
+                stop = __shfl((int)c.x, 8, 64); /* chunk 8: the stop word */
                 fresh = s0 != last && __all(t >= 8 || (c.x == s0 && c.z == s0));
                 if (t < 8) {
                     const uint32_t k = t >> 1;
@@ -731,7 +735,8 @@ namespace {
 
 struct Worker {
     std::mutex mu;
-    int state = 0;             /* 0 unknown, 1 usable, -1 disabled */
+    int state = 0;             /* 0 unknown, 1 usable, -1 disabled, -2 draining (worker_abandon) */
+    uint32_t launches = 0;     /* debug: kernels launched (noise_aead_debug_worker_launches) */
     int launch_fails = 0;      /* consecutive failed launches (3 disable the worker) */
     WorkerSlot *slot = nullptr; /* host view */
     WorkerSlot *dslot = nullptr; /* device view */
@@ -747,6 +752,13 @@ struct Worker {
     hipStream_t stream = nullptr;
     uint32_t seq = 0;
     bool launched = false;     /* written under mu, read by park() with atomics */
+    /* the AES-GCM contexts (host copies) sent to the running worker, whose
+       LDS cache may hold them: only a worker that was sent a context is
+       parked when the state is freed; past kCtxHist distinct
+       ones since its launch, any free parks it */
+    static constexpr int kCtxHist = 8;
+    const void *ctx_hist[kCtxHist] = {};
+    uint32_t ctx_n = 0;        /* written under mu, read by forget() with atomics */
 };
 
 constexpr int kMaxDev = 64;
@@ -810,21 +822,74 @@ constexpr uint64_t LIFETIME_TICKS = 500000000; /* 5 s */
    the launch path and the worker is not used again. */
 constexpr uint64_t WAIT_LIMIT_NS = 2000000000ull; /* 2 s */
 
-/* the header's stop field: chunk 2 word 3 (host memory), chunk 5 word 1 (device) */
-uint32_t *stop_word(Worker &w) { return w.vram ? &w.req[4 * 5 + 1] : &w.req[4 * 2 + 3]; }
+/* the stop word: chunk 4 of the host slot, chunk 8 of the device request
+   area — a chunk of its own, apart from the request header the calls
+   rewrite */
+uint32_t *stop_word(Worker &w) { return w.vram ? &w.req[4 * 8] : &w.req[4 * 4]; }
 
-/* Ask every launched worker of device dev to leave (no wait).  A worker
-   leaving scrubs its LDS; a request racing with the stop is either served or
-   seen by its caller as `exiting` (the caller then starts a new worker). */
+/* Ask a launched worker to leave (no wait).  A worker leaving scrubs its
+   LDS; a request racing with the stop is either served or seen by its
+   caller as `exiting` (the caller then starts a new worker).  The stop word
+   has a chunk of its own, so no request header written meanwhile can undo
+   it. */
+void park_worker(Worker &w)
+{
+    if (__atomic_load_n(&w.launched, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
+        _mm_sfence();
+    }
+}
+
 void park_device(int dev)
 {
-    for (int i = 0; i < kWorkersPerDev; ++i) {
-        Worker &w = g_worker[dev][i];
-        if (__atomic_load_n(&w.launched, __ATOMIC_ACQUIRE)) {
-            __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
-            _mm_sfence();
-        }
-    }
+    for (int i = 0; i < kWorkersPerDev; ++i) park_worker(g_worker[dev][i]);
+}
+
+/* Did worker w (maybe) receive AES-GCM context h since its launch? */
+bool worker_saw_ctx(const Worker &w, const void *h)
+{
+    const uint32_t n = __atomic_load_n(&w.ctx_n, __ATOMIC_ACQUIRE);
+    if (n > (uint32_t)Worker::kCtxHist) return true; /* history overflowed */
+    for (uint32_t i = 0; i < n; ++i)
+        if (__atomic_load_n(&w.ctx_hist[i], __ATOMIC_RELAXED) == h) return true;
+    return false;
+}
+
+/* (under w.mu) record that context h goes to worker w */
+void worker_note_ctx(Worker &w, const void *h)
+{
+    const uint32_t n = w.ctx_n;
+    if (n > (uint32_t)Worker::kCtxHist) return;
+    for (uint32_t i = 0; i < n; ++i)
+        if (w.ctx_hist[i] == h) return;
+    if (n < (uint32_t)Worker::kCtxHist) __atomic_store_n(&w.ctx_hist[n], h, __ATOMIC_RELAXED);
+    __atomic_store_n(&w.ctx_n, n + 1, __ATOMIC_RELEASE);
+}
+
+/* A request the worker did not answer within WAIT_LIMIT_NS (under w.mu):
+   the worker is asked to leave and the request's header is made
+   unservable — its first chunk no longer agrees with the others — so a late
+   worker cannot take it; the worker is drained (state -2) and made usable
+   again once its stream is idle (worker_recover), when its result area is
+   scrubbed once more in case a late worker wrote it. */
+void worker_abandon(Worker &w, uint32_t k)
+{
+    __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
+    const uint32_t bad = k ^ 0x80000000u;
+    const __m128i c = w.vram ? _mm_set_epi32(0, (int)bad, 0, (int)bad) : _mm_set_epi32(0, 0, 0, (int)bad);
+    _mm_store_si128((__m128i *)w.req, c);
+    _mm_sfence();
+    w.state = -2;
+}
+
+/* (under w.mu) a drained worker whose stream has gone idle: results
+   scrubbed, usable again (relaunched by the next call) */
+void worker_recover(Worker &w)
+{
+    if (w.state != -2 || hipStreamQuery(w.stream) != hipSuccess) return;
+    explicit_bzero(w.out, WORKER_DATA);
+    __atomic_store_n(&w.launched, false, __ATOMIC_RELEASE);
+    w.state = 1;
 }
 
 void worker_stop_all()
@@ -833,10 +898,11 @@ void worker_stop_all()
         for (int i = 0; i < kWorkersPerDev; ++i) {
             Worker &w = g_worker[d][i];
             std::lock_guard<std::mutex> lk(w.mu);
-            if (w.state != 1 || !w.launched) continue;
+            if ((w.state != 1 && w.state != -2) || !w.launched) continue;
             __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
             _mm_sfence();
             (void)hipStreamSynchronize(w.stream);
+            if (w.state == -2) explicit_bzero(w.out, WORKER_DATA); /* a late worker's results */
             __atomic_store_n(&w.launched, false, __ATOMIC_RELEASE);
         }
 }
@@ -882,15 +948,16 @@ int worker_setup(Worker &w, int dev)
     w.dout = w.dtail + tail_bytes;
     w.req = w.slot->c0;
     w.dreq = w.dslot->c0;
-    /* device-memory request: 8 header chunks (128 B), the stamped chunks, then the raw tail */
-    const size_t vbytes = 128 + in_bytes + VWORKER_TAIL + 64;
+    /* device-memory request: 8 header chunks and the stop chunk (256 B), the
+       stamped chunks, then the raw tail */
+    const size_t vbytes = 256 + in_bytes + VWORKER_TAIL + 64;
     if (vram_wanted(dev) && hipExtMallocWithFlags(&w.vbase, vbytes, hipDeviceMallocFinegrained) == hipSuccess) {
         memset(w.vbase, 0, vbytes); /* through the BAR mapping */
         _mm_sfence();
         w.vram = true;
         w.req = (uint32_t *)w.vbase;
         w.dreq = (const uint32_t *)w.vbase;
-        w.in = w.din = (uint4 *)((uint8_t *)w.vbase + 128);
+        w.in = w.din = (uint4 *)((uint8_t *)w.vbase + 256);
         w.tail = w.dtail = (uint8_t *)(w.in + WORKER_SPEC);
     }
     if (worker_stream_prio() == 0) {
@@ -941,6 +1008,7 @@ int worker_launch(Worker &w)
     __atomic_store_n(&w.slot->exiting, 0u, __ATOMIC_RELEASE);
     __atomic_store_n(stop_word(w), 0u, __ATOMIC_RELEASE);
     _mm_sfence();
+    __atomic_store_n(&w.ctx_n, 0u, __ATOMIC_RELEASE); /* a fresh worker caches nothing */
     hipLaunchKernelGGL(aead_worker, dim3(1), dim3(256), 0, w.stream, w.dslot, w.dreq, (const uint4 *)w.din,
                        w.vram ? 1u : 0u, (const uint8_t *)w.dtail, w.dout, w.seq, idle_ticks(), LIFETIME_TICKS);
     if (hipGetLastError() != hipSuccess) {
@@ -948,6 +1016,7 @@ int worker_launch(Worker &w)
         return NOISE_ERROR_NOT_APPLICABLE;
     }
     w.launch_fails = 0;
+    __atomic_add_fetch(&w.launches, 1u, __ATOMIC_RELAXED);
     __atomic_store_n(&w.launched, true, __ATOMIC_RELEASE);
     return NOISE_ERROR_NONE;
 }
@@ -963,6 +1032,7 @@ Worker *claim_worker(int dev, std::unique_lock<std::mutex> &lk)
         Worker &w = g_worker[dev][(t_pref + i) % nw];
         std::unique_lock<std::mutex> l(w.mu, std::try_to_lock);
         if (!l.owns_lock()) continue;
+        worker_recover(w);
         if (worker_setup(w, dev) != 1) continue;
         lk = std::move(l);
         return &w;
@@ -970,6 +1040,7 @@ Worker *claim_worker(int dev, std::unique_lock<std::mutex> &lk)
     for (int i = 0; i < nw; ++i) {
         Worker &w = g_worker[dev][(t_pref + i) % nw];
         std::unique_lock<std::mutex> l(w.mu);
+        worker_recover(w);
         if (worker_setup(w, dev) != 1) continue;
         lk = std::move(l);
         return &w;
@@ -1004,11 +1075,16 @@ NA_HIDDEN void worker_park_for_batch(uint32_t workgroups)
     if (workgroups >= (uint32_t)cus && park_enabled()) park_device(dev);
 }
 
-/* A state's AES-GCM context is being freed: every worker that may hold it in
-   its LDS cache leaves (and scrubs its LDS on the way out). */
-extern "C" NA_HIDDEN void na_worker_forget_ctx(void)
+/* A state's AES-GCM context (its pinned host copy h_ctx) is being freed:
+   every worker that was sent it since its launch — and so may hold it in its
+   LDS cache — leaves, scrubbing its LDS on the way out; the others stay. */
+extern "C" NA_HIDDEN void na_worker_forget_ctx(const void *h_ctx)
 {
-    for (int d = 0; d < kMaxDev; ++d) park_device(d);
+    for (int d = 0; d < kMaxDev; ++d)
+        for (int i = 0; i < kWorkersPerDev; ++i) {
+            Worker &w = g_worker[d][i];
+            if (worker_saw_ctx(w, h_ctx)) park_worker(w);
+        }
 }
 
 namespace {
@@ -1066,6 +1142,7 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     void *d_hctx = nullptr;
     if (h_ctx && hipHostGetDevicePointer(&d_hctx, (void *)h_ctx, 0) != hipSuccess)
         return NOISE_ERROR_NOT_APPLICABLE;
+    if (h_ctx) worker_note_ctx(w, h_ctx);
     const size_t ad_pad = (ad_len + 15) & ~(size_t)15;
     WorkerSlot *s = w.slot;
     if (!w.launched || __atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE)) {
@@ -1149,8 +1226,8 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
                 break;
             }
         }
-        if (host_ns() - h2 > WAIT_LIMIT_NS) { /* lost: never used again */
-            w.state = -1;
+        if (host_ns() - h2 > WAIT_LIMIT_NS) { /* no answer: drained, then reused */
+            worker_abandon(w, k);
             st = NOISE_ERROR_NOT_APPLICABLE;
             break;
         }
@@ -1217,6 +1294,17 @@ extern "C" int noise_aead_debug_workers_resident(void)
         std::lock_guard<std::mutex> lk(w.mu);
         if (w.state == 1 && w.launched && hipStreamQuery(w.stream) == hipErrorNotReady) ++n;
     }
+    return n;
+}
+
+/* Test hook: worker kernels launched on the current device so far (a
+   parked worker that is called again is relaunched). */
+extern "C" unsigned noise_aead_debug_worker_launches(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
+    unsigned n = 0;
+    for (int i = 0; i < kWorkersPerDev; ++i) n += __atomic_load_n(&g_worker[dev][i].launches, __ATOMIC_RELAXED);
     return n;
 }
 

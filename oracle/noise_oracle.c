@@ -439,6 +439,51 @@ void oracle_seal_uniform(int cipher, const uint8_t *keys,
     }
 }
 
+/* oracle_seal_uniform with associated data: record i's AD at ad + i * ad_stride */
+void oracle_seal_uniform_ad(int cipher, const uint8_t *keys,
+                            const uint64_t *nonce_base, uint32_t recs_per_state,
+                            const uint8_t *in, size_t in_stride,
+                            uint8_t *out, size_t out_stride,
+                            uint32_t len, uint32_t count,
+                            const uint8_t *ad, size_t ad_stride, uint32_t ad_len)
+{
+    for (uint32_t i = 0; i < count; ++i) {
+        uint32_t s = i / recs_per_state;
+        uint8_t *o = out + (size_t)i * out_stride;
+        memmove(o, in + (size_t)i * in_stride, len);
+        oracle_aead_encrypt(cipher, keys + 32 * (size_t)s,
+                            nonce_base[s] + (i % recs_per_state),
+                            ad_len ? ad + (size_t)i * ad_stride : 0, ad_len, o, len);
+    }
+}
+
+/* A ragged batch (the 48-byte NoiseAeadRecord descriptors of
+   include/noise_aead_hip.h): record i sealed from in + in_off to
+   out + out_off (ct || tag) with the key key_idx[i] of keys and its own
+   nonce and AD; records longer than 65519 bytes are skipped, as the device
+   kernels refuse them. */
+void oracle_seal_ragged(int cipher, const uint8_t *keys, const uint32_t *key_idx,
+                        const uint8_t *recs, uint32_t count,
+                        const uint8_t *in, uint8_t *out, const uint8_t *ad)
+{
+    for (uint32_t i = 0; i < count; ++i) {
+        const uint8_t *d = recs + 48 * (size_t)i;
+        uint64_t in_off, out_off, nonce, ad_off;
+        uint32_t len, ad_len;
+        memcpy(&in_off, d, 8);
+        memcpy(&out_off, d + 8, 8);
+        memcpy(&nonce, d + 16, 8);
+        memcpy(&ad_off, d + 32, 8);
+        memcpy(&len, d + 40, 4);
+        memcpy(&ad_len, d + 44, 4);
+        if (len > 65535 - 16) continue;
+        uint8_t *o = out + out_off;
+        memmove(o, in + in_off, len);
+        oracle_aead_encrypt(cipher, keys + 32 * (size_t)key_idx[i], nonce,
+                            ad_len ? ad + ad_off : 0, ad_len, o, len);
+    }
+}
+
 void oracle_open_uniform(int cipher, const uint8_t *keys,
                          const uint64_t *nonce_base, uint32_t recs_per_state,
                          const uint8_t *in, size_t in_stride,

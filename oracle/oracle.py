@@ -67,6 +67,9 @@ class Oracle:
                                           u8p, sz, C.c_uint32, C.c_uint32]
         L.oracle_open_uniform.argtypes = [C.c_int, u8p, u64p, C.c_uint32, u8p, sz,
                                           u8p, sz, C.c_uint32, C.c_uint32, u8p]
+        L.oracle_seal_uniform_ad.argtypes = [C.c_int, u8p, u64p, C.c_uint32, u8p, sz,
+                                             u8p, sz, C.c_uint32, C.c_uint32, u8p, sz, C.c_uint32]
+        L.oracle_seal_ragged.argtypes = [C.c_int, u8p, u8p, u8p, C.c_uint32, u8p, u8p, u8p]
         L.oracle_chacha20_block.argtypes = [u8p, C.c_uint64, C.c_uint64, u8p]
         L.oracle_poly1305.argtypes = [u8p, u8p, sz, u8p]
         L.oracle_aes256_encrypt_block.argtypes = [u8p, u8p, u8p]
@@ -152,6 +155,18 @@ class Oracle:
         self.L.oracle_seal_uniform(cipher, keys.ctypes.data, nonce_base.ctypes.data,
                                    rps, inp.ctypes.data, in_stride, out.ctypes.data,
                                    out_stride, length, count)
+
+    def seal_uniform_ad(self, cipher, keys, nonce_base, rps, inp, in_stride, out,
+                        out_stride, length, count, ad, ad_stride, ad_len):
+        self.L.oracle_seal_uniform_ad(cipher, keys.ctypes.data, nonce_base.ctypes.data,
+                                      rps, inp.ctypes.data, in_stride, out.ctypes.data,
+                                      out_stride, length, count, ad.ctypes.data, ad_stride, ad_len)
+
+    def seal_ragged(self, cipher, keys, key_idx, recs, inp, out, ad):
+        """recs: structured array of the 48-B descriptors; key_idx: uint32 per record"""
+        self.L.oracle_seal_ragged(cipher, keys.ctypes.data, key_idx.ctypes.data,
+                                  recs.ctypes.data, len(recs), inp.ctypes.data, out.ctypes.data,
+                                  ad.ctypes.data)
 
     def open_uniform(self, cipher, keys, nonce_base, rps, inp, in_stride, out,
                      out_stride, length, count, status):

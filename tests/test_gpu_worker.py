@@ -200,3 +200,16 @@ def test_freed_aes_state_clears_worker_cache(gpu):
                         "--free-check"], env=dict(os.environ, **env), timeout=110, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert float(r.stdout.split("left_ms")[-1].split()[0]) >= 0
+
+
+def test_free_beside_concurrent_caller_parks_only_that_worker(gpu):
+    """freeing an AES-GCM state parks the worker that was sent its
+    context even while another thread keeps writing request headers (the
+    stop word has a chunk of its own), and only that worker — the other
+    thread's worker, which never saw the context, is not relaunched."""
+    env = {"NOISE_AEAD_DEBUG_WORKER_IDLE_MS": "10000", "GPU_MAX_HW_QUEUES": "2"}
+    r = subprocess.run([sys.executable, "-u", os.path.join(os.path.dirname(__file__), "worker_mode_check.py"),
+                        "--free-concurrent"], env=dict(os.environ, **env), timeout=110, capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "parked_ok 1" in r.stdout

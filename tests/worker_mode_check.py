@@ -80,5 +80,62 @@ def free_check():
     return 0 if left else 1
 
 
+def free_concurrent():
+    """--free-concurrent (run with GPU_MAX_HW_QUEUES=2 and
+    NOISE_AEAD_DEBUG_WORKER_IDLE_MS=10000): thread A keeps making ChaChaPoly
+    single calls (its worker stays resident, its request headers keep being
+    written); the main thread's AES-GCM state S, used once from the main
+    thread (the other worker caches its context), is freed.  The worker that
+    was sent S's context must leave — its stop word is no longer part of the
+    header A's calls rewrite — and A's worker, which never saw
+    S's context, must stay (no relaunch of it).  Prints "parked_ok 1"."""
+    import threading
+    import time
+    lib = aead.lib()
+    lib.noise_aead_debug_workers_resident.restype = int
+    lib.noise_aead_debug_worker_launches.restype = int
+    stop = [False]
+    errs = []
+    started = threading.Event()
+
+    def caller():
+        _, cs = aead.CipherState.new_by_id(0x4301)
+        cs.init_key(bytes(range(32)))
+        n = 0
+        while not stop[0]:
+            if len(cs.seal(bytes(1400))) != 1416:
+                errs.append("seal")
+            n += 1
+            if n == 50:
+                started.set()
+        cs.free()
+
+    th = threading.Thread(target=caller)
+    th.start()
+    started.wait(30)
+    _, st = aead.CipherState.new_by_id(0x4302)
+    assert st.init_key(bytes(range(1, 33))) == 0
+    st.seal(bytes(100))
+    time.sleep(0.05)
+    res0, l0 = lib.noise_aead_debug_workers_resident(), lib.noise_aead_debug_worker_launches()
+    st.free()
+    t0 = time.time()
+    while lib.noise_aead_debug_workers_resident() >= res0 and time.time() - t0 < 0.5:
+        time.sleep(0.001)
+    res1 = lib.noise_aead_debug_workers_resident()
+    time.sleep(0.1)
+    l1 = lib.noise_aead_debug_worker_launches()
+    stop[0] = True
+    th.join()
+    ok = res0 == 2 and res1 == 1 and l1 == l0 and not errs
+    print("resident", res0, res1, "launches", l0, l1, "errs", errs[:3])
+    print("parked_ok", 1 if ok else 0)
+    return 0 if ok else 1
+
+
 if __name__ == "__main__":
-    sys.exit(free_check() if "--free-check" in sys.argv else main())
+    if "--free-check" in sys.argv:
+        sys.exit(free_check())
+    if "--free-concurrent" in sys.argv:
+        sys.exit(free_concurrent())
+    sys.exit(main())
