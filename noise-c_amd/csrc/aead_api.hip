@@ -81,24 +81,33 @@ bool solo_enabled()
     return on;
 }
 
-/* Round 5: a standalone job of SOLO_MIN_RECORDS <= n < SOLO_MIN_STANDALONE
-   FAST records takes two segments per record (chachapoly_seg.hip: 2048 waves
-   at 64 Ki records, two per SIMD, each record's Poly1305 as two chains
-   joined by r^e).  NOISE_AEAD_SEG=0 keeps the four-lane staged kernels
-   there (A/B runs). */
-bool seg_enabled()
+/* The segmented kernels (chachapoly_seg.hip).  NOISE_AEAD_SEG=0 turns them
+   off (the ragged path then keeps the windowed 8-lane kernels); =2 also
+   makes a standalone job of SOLO_MIN_RECORDS <= n < SOLO_MIN_STANDALONE FAST
+   records take two segments per record (2048 waves at 64 Ki records, two
+   per SIMD).  Round 5 measured that shape slower than the four-lane staged
+   kernel it would replace — C2 standalone seal 73 vs 63 us
+   (profiles/r05/seg2_standalone_ab.jsonl): 7 % fewer VALU instructions than
+   four lanes but 16 % more than one lane per record (the split's second
+   chain, r^e, the 24th block slot), and two waves of six steps per SIMD
+   issue 11 % slower than the duplex launch's seal + open pair — so the
+   default keeps four lanes there.  lanes_per_record = 2 on a FAST layout
+   always takes it. */
+int seg_mode()
 {
-    static const bool on = [] {
+    static const int v = [] {
         const char *e = getenv("NOISE_AEAD_SEG");
-        return !(e && e[0] == '0');
+        return e ? (e[0] == '0' ? 0 : (e[0] == '2' ? 2 : 1)) : 1;
     }();
-    return on;
+    return v;
 }
+
+bool seg_enabled() { return seg_mode() != 0; }
 
 int standalone_lanes(uint32_t n)
 {
     if (n >= SOLO_MIN_STANDALONE) return 1;
-    return seg_enabled() ? 2 : 0;
+    return seg_mode() == 2 ? 2 : 0;
 }
 
 int uniform_lanes(const NoiseAeadUniform *j, bool open, bool duplex)

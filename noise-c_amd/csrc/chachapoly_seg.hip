@@ -165,6 +165,16 @@ NA_DEV bool seg_store_ok(uint32_t off, uint32_t sl)
     return !((sl >> 31) && off < 64u) && off + 16u <= (sl & 0x7fffffffu);
 }
 
+/* rec_store16 to an address held as an integer, as a global (not flat)
+   store: a flat store also counts in lgkmcnt, so every later LDS wait would
+   wait for it too */
+typedef __attribute__((address_space(1))) na_u32x4 seg_gvec;
+NA_DEV void seg_store16(uint64_t a, const uint4 &q)
+{
+    const na_u32x4 v = {q.x, q.y, q.z, q.w};
+    __builtin_nontemporal_store(v, (seg_gvec *)(uintptr_t)a);
+}
+
 struct SegIOL {
     SegOwner *tab; /* this wave's 64 owners (LDS) */
     NA_DEV void init(const SegLane &q, uint32_t lane)
@@ -186,13 +196,23 @@ struct SegIOL {
     }
     NA_DEV void store(uint32_t lane, uint32_t m, const uint4 *t, uint32_t okm) const
     {
+        /* the tile values and owner entries first, one wait, then the stores
+           (a read and its wait inside each store's branch serialised them) */
         const uint32_t off = 128u * m + 16u * solo_chunk(lane);
+        uint4 v[8];
+        uint64_t dst[8];
+        uint32_t ok = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const SegOwner &o = tab[8 * i + (lane >> 3)];
-            if (((okm >> i) & 1) && o.hi && seg_store_ok(off, o.sl) && SEG_OK(o.out + off, 16, 2, m << 16 | lane << 8 | i))
-                rec_store16((uint8_t *)(uintptr_t)(o.out + off), t[64 * i + lane]);
+            v[i] = t[64 * i + lane];
+            dst[i] = o.out + off;
+            ok |= (o.hi && seg_store_ok(off, o.sl) ? 1u : 0u) << i;
         }
+        ok &= okm;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (((ok >> i) & 1) && SEG_OK(dst[i], 16, 2, m << 16 | lane << 8 | i)) seg_store16(dst[i], v[i]);
     }
 };
 
@@ -203,6 +223,7 @@ struct SegIOU {
     int64_t lin, lout; /* this lane's owner: (lane/16) strides + 64 (b0 - 1) */
     uint32_t hi, sl;   /* its geometry (every record has the same length) */
     uint32_t livem;    /* bit i: owner record rec0 + 4i + lane/16 exists */
+    bool full;         /* wave-uniform: all 32 records of the wave exist */
     NA_DEV void init(const UniformArgs &a, uint32_t rec0, const SegLane &q, uint32_t lane)
     {
         in = a.in + (size_t)rec0 * a.in_stride;
@@ -224,11 +245,18 @@ struct SegIOU {
         livem = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) livem |= (rec0 + 4u * i + (lane >> 4) < a.n_records ? 1u : 0u) << i;
+        full = rec0 + 32u <= a.n_records;
     }
     NA_DEV void dma(uint32_t lane, uint32_t m, uint4 *t) const
     {
         const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)t);
         const uint32_t off = seg_dma_off(m, solo_chunk(lane), hi, sl);
+        if (full) { /* wave-uniform: no per-instruction predicate */
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (hi) dma16_asm(in + (size_t)(4 * i) * in_stride + lin + off, base + 1024u * (uint32_t)i);
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             if (((livem >> i) & 1) && hi)
@@ -238,10 +266,18 @@ struct SegIOU {
     {
         const uint32_t off = 128u * m + 16u * solo_chunk(lane);
         if (!hi || !seg_store_ok(off, sl)) return;
+        uint4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = t[64 * i + lane]; /* all reads, one wait */
+        if (full && okm == 0xffu) { /* wave-uniform: every owner stores */
+#pragma unroll
+            for (int i = 0; i < 8; ++i) rec_store16(out + (size_t)(4 * i) * out_stride + lout + off, v[i]);
+            return;
+        }
+        const uint32_t ok = livem & okm;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            if (((livem & okm) >> i) & 1)
-                rec_store16(out + (size_t)(4 * i) * out_stride + lout + off, t[64 * i + lane]);
+            if ((ok >> i) & 1) rec_store16(out + (size_t)(4 * i) * out_stride + lout + off, v[i]);
     }
 };
 
@@ -293,97 +329,116 @@ NA_DEV void seg_bcast_r(const SegLane &q, uint32_t lane, const uint32_t kw[4], R
     r = r32_from_key(rw[0], rw[1], rw[2], rw[3]);
 }
 
-/* Data unit j of this lane: w holds the tile's unit on entry and leaves
-   with what the tile takes (SEAL: CT; OPEN1 / DEC: plaintext); c receives
-   the unit's Poly1305 input (the CT, masked past len) and the return value
-   is its number of Poly blocks (SEAL, OPEN1). */
-template <int MODE>
-NA_DEV uint32_t seg_xor(const SegLane &q, uint32_t j, uint32_t w[16], const uint32_t x[16], uint32_t c[16],
-                        bool ok)
+/* Data unit j of this lane, in solo_pass's order and registers: w holds the
+   tile's unit on entry and leaves with what the tile takes (SEAL: CT;
+   OPEN1 / DEC: plaintext; past len the bytes are never stored).  SEAL /
+   OPEN1 chain the unit's Poly1305 blocks (the CT, zero past len) unless
+   DEFER: then w leaves as that Poly input and the caller chains it and
+   (OPEN1) XORs x itself — step 0, before r has arrived. */
+template <int MODE, bool DEFER = false>
+NA_DEV void seg_data(const SegLane &q, uint32_t j, uint32_t w[16], const uint32_t x[16], const R32 &r,
+                     P32 &h, bool ok, uint32_t &nbp)
 {
     const bool last = j == q.J - 1;
+    nbp = last ? (q.tail + 15) / 16 : 4u;
     if constexpr (MODE == SEG_OPEN1) {
+        if (last) mask_unit(w, q.tail);
+        if constexpr (DEFER) return;
+        p32_unit(h, r, w, nbp);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            c[i] = w[i];
-            w[i] ^= x[i];
-        }
+        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
         if (last && SEG_OK(q.dst + 64 * j, q.tail, 3, j)) seg_last_out(q.dst + 64 * j, q.tail, w);
     } else {
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] ^= x[i];
-        if (last && (MODE == SEG_SEAL || ok) && SEG_OK(q.dst + 64 * j, q.tail, 3, j)) seg_last_out(q.dst + 64 * j, q.tail, w);
-        if constexpr (MODE == SEG_SEAL) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) c[i] = w[i];
+        if (last) {
+            if ((MODE == SEG_SEAL || ok) && SEG_OK(q.dst + 64 * j, q.tail, 3, j)) seg_last_out(q.dst + 64 * j, q.tail, w);
+            if (MODE == SEG_SEAL) mask_unit(w, q.tail);
         }
+        if constexpr (MODE == SEG_SEAL && !DEFER) p32_unit(h, r, w, nbp);
     }
-    if (last) {
-        mask_unit(c, q.tail);
-        return (q.tail + 15) / 16;
-    }
-    return 4;
 }
 
-/* One pass over the wave's segments, two blocks per step (the order of
-   solo_pass: wait for the DMA a step old, read the tile, store the previous
-   step from the other tile, issue the next DMA, compute).  SEAL / OPEN1:
-   in step 0 the leader's first block is the key block: slot 0 is XORed (its
-   Poly input kept), r reaches every lane from its record's leader, the
-   leader absorbs the AD, then slot 0's Poly and slot 1.  DEC
+/* Step m of a pass (the order of solo_pass: wait for the DMA a step old,
+   read the tile, store the previous step from the other tile, issue the
+   next DMA, compute).  FIRST (SEAL / OPEN1 step 0): the leader's first
+   block is the key block — slot 0's block is computed and its unit XORed /
+   kept, r reaches every lane from its record's leader, the leader absorbs
+   the AD, then slot 0's Poly1305 and slot 1.  Step 0 is peeled out of the
+   loop: inside it, its branch doubled the loop's register allocation (256
+   VGPRs and spills against 158). */
+template <int MODE, bool PRIO, bool FIRST, class IO>
+NA_DEV void seg_step(const SegLane &q, const IO &io, uint32_t lane, uint32_t m, uint32_t S, uint4 *tiles,
+                     const uint32_t key[8], const ChaPre &pre, R32 &r, uint32_t rw[4], uint32_t s[4],
+                     P32 &h, uint32_t okm, bool ok)
+{
+    uint4 *cur = tiles + SOLO_TILE * (m & 1), *nxt = tiles + SOLO_TILE * ((m + 1) & 1);
+    uint32_t wu[2][16];
+    solo_wait();
+    solo_get(cur, lane, 0, wu[0]);
+    solo_get(cur, lane, 1, wu[1]);
+    if (!FIRST && m >= 1) io.store(lane, m - 1, nxt, okm);
+    __builtin_amdgcn_wave_barrier();
+    if (m + 1 < S) io.dma(lane, m + 1, nxt);
+    if (PRIO) prio_by_progress(m, S);
+    if constexpr (FIRST) {
+        uint32_t x[16], kw[4] = {0, 0, 0, 0}, nb0 = 0;
+        const bool d0 = q.nb > 0 && q.b0 != 0; /* slot 0 holds data */
+        if (q.nb > 0) {
+            chacha20_block_pre(key, pre, q.b0, q.n_lo, q.n_hi, x);
+            if (q.b0 == 0) {
+                kw[0] = x[0]; kw[1] = x[1]; kw[2] = x[2]; kw[3] = x[3];
+                s[0] = x[4]; s[1] = x[5]; s[2] = x[6]; s[3] = x[7];
+            } else {
+                seg_data<MODE, true>(q, q.b0 - 1, wu[0], x, r, h, ok, nb0);
+            }
+        }
+        seg_bcast_r(q, lane, kw, r, rw);
+        if (q.b0 == 0 && q.live && q.ad_len && SEG_OK(q.ad, q.ad_len, 4, 0)) p32_ad(h, r, q.ad, q.ad_len);
+        if (d0) {
+            p32_unit(h, r, wu[0], nb0);
+            if (MODE == SEG_OPEN1) {
+                const uint32_t j = q.b0 - 1;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) wu[0][i] ^= x[i];
+                if (j == q.J - 1 && SEG_OK(q.dst + 64 * j, q.tail, 3, j)) seg_last_out(q.dst + 64 * j, q.tail, wu[0]);
+            }
+            solo_put(cur, lane, 0, wu[0]);
+        }
+        if (q.nb > 1) {
+            uint32_t x1[16], nbp;
+            chacha20_block_pre(key, pre, q.b0 + 1, q.n_lo, q.n_hi, x1);
+            seg_data<MODE>(q, q.b0, wu[1], x1, r, h, ok, nbp);
+            solo_put(cur, lane, 1, wu[1]);
+        }
+    } else {
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t blk = q.b0 + 2 * m + u;
+            if (2 * m + u < q.nb && blk != 0 && (MODE != SEG_DEC || ok)) {
+                uint32_t x[16], nbp;
+                chacha20_block_pre(key, pre, blk, q.n_lo, q.n_hi, x);
+                seg_data<MODE>(q, blk - 1, wu[u], x, r, h, ok, nbp);
+                solo_put(cur, lane, u, wu[u]);
+            }
+        }
+    }
+}
+
+/* One pass over the wave's segments, two blocks per step.  DEC
    (verify-first, r known): key stream only; block 0 skipped. */
 template <int MODE, bool PRIO, class IO>
 NA_DEV void seg_pass(const SegLane &q, const IO &io, uint32_t lane, uint32_t S, uint4 *tiles,
                      const uint32_t key[8], const ChaPre &pre, R32 &r, uint32_t rw[4], uint32_t s[4],
                      P32 &h, uint32_t okm, bool ok)
 {
-    for (uint32_t m = 0; m < S; ++m) {
-        uint4 *cur = tiles + SOLO_TILE * (m & 1), *nxt = tiles + SOLO_TILE * ((m + 1) & 1);
-        uint32_t wu[2][16];
-        solo_wait();
-        solo_get(cur, lane, 0, wu[0]);
-        solo_get(cur, lane, 1, wu[1]);
-        if (m >= 1) io.store(lane, m - 1, nxt, okm);
-        __builtin_amdgcn_wave_barrier();
-        if (m + 1 < S) io.dma(lane, m + 1, nxt);
-        if (PRIO) prio_by_progress(m, S);
-        if (MODE != SEG_DEC && m == 0) {
-            uint32_t c0[16], kw[4] = {0, 0, 0, 0}, nb0 = 0;
-            if (q.nb > 0) {
-                uint32_t x[16];
-                chacha20_block_pre(key, pre, q.b0, q.n_lo, q.n_hi, x);
-                if (q.b0 == 0) {
-                    kw[0] = x[0]; kw[1] = x[1]; kw[2] = x[2]; kw[3] = x[3];
-                    s[0] = x[4]; s[1] = x[5]; s[2] = x[6]; s[3] = x[7];
-                } else {
-                    nb0 = seg_xor<MODE>(q, q.b0 - 1, wu[0], x, c0, ok);
-                    solo_put(cur, lane, 0, wu[0]);
-                }
-            }
-            seg_bcast_r(q, lane, kw, r, rw);
-            if (q.b0 == 0 && q.live && q.ad_len && SEG_OK(q.ad, q.ad_len, 4, 0)) p32_ad(h, r, q.ad, q.ad_len);
-            if (nb0) p32_unit(h, r, c0, nb0);
-            if (q.nb > 1) {
-                uint32_t x[16], c[16];
-                chacha20_block_pre(key, pre, q.b0 + 1, q.n_lo, q.n_hi, x);
-                const uint32_t nbp = seg_xor<MODE>(q, q.b0, wu[1], x, c, ok);
-                p32_unit(h, r, c, nbp);
-                solo_put(cur, lane, 1, wu[1]);
-            }
-            continue;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < 2; ++u) {
-            const uint32_t blk = q.b0 + 2 * m + u;
-            if (2 * m + u < q.nb && blk != 0 && (MODE != SEG_DEC || ok)) {
-                uint32_t x[16], c[16];
-                chacha20_block_pre(key, pre, blk, q.n_lo, q.n_hi, x);
-                const uint32_t nbp = seg_xor<MODE>(q, blk - 1, wu[u], x, c, ok);
-                if (MODE != SEG_DEC) p32_unit(h, r, c, nbp);
-                solo_put(cur, lane, u, wu[u]);
-            }
-        }
+    uint32_t m0 = 0;
+    if (MODE != SEG_DEC && S) {
+        seg_step<MODE, PRIO, true>(q, io, lane, 0u, S, tiles, key, pre, r, rw, s, h, okm, ok);
+        m0 = 1;
     }
+    for (uint32_t m = m0; m < S; ++m)
+        seg_step<MODE, PRIO, false>(q, io, lane, m, S, tiles, key, pre, r, rw, s, h, okm, ok);
     if (S) {
         __builtin_amdgcn_wave_barrier();
         io.store(lane, S - 1, tiles + SOLO_TILE * ((S - 1) & 1), okm);

@@ -30,7 +30,11 @@ CONFIGS = {
     "c2": dict(cipher=CHACHA, records=65536, len=1400, states=1),
     "c3": dict(cipher=AES, records=65536, len=1400, states=1),
     "c4": dict(cipher=CHACHA, records=1048576, len=1400, states=4096),
+    # noise-c's tests/performance shape (bench.py "perf"): 1024-B records with
+    # 32 B of AD each, the AD the SplitMix64 stream of seed 0x6164
+    "perf": dict(cipher=CHACHA, records=65536, len=1024, states=1, ad=32),
 }
+SEED_AD = 0x6164
 
 
 def stride(n):
@@ -44,9 +48,14 @@ def digests(o, name, cfg):
     nb = np.zeros(S, dtype=np.uint64)
     pt = np.frombuffer(o.fill(SEED_PT, N * ins, 0), dtype=np.uint8).copy()
     ct = np.zeros(N * outs, dtype=np.uint8)
-    o.seal_uniform(cfg["cipher"], keys, nb, N // S, pt, ins, ct, outs, L, N)
+    AD = cfg.get("ad", 0)
+    if AD:
+        ad = np.frombuffer(o.fill(SEED_AD, N * AD, 0), dtype=np.uint8).copy()
+        o.seal_uniform_ad(cfg["cipher"], keys, nb, N // S, pt, ins, ct, outs, L, N, ad, AD, AD)
+    else:
+        o.seal_uniform(cfg["cipher"], keys, nb, N // S, pt, ins, ct, outs, L, N)
     return dict(cipher=cfg["cipher"], records=N, len=L, states=S, recs_per_state=N // S,
-                in_stride=ins, out_stride=outs,
+                in_stride=ins, out_stride=outs, ad=AD,
                 pt_sha256=hashlib.sha256(pt.reshape(N, ins)[:, :L].tobytes()).hexdigest(),
                 sealed_sha256=hashlib.sha256(ct.reshape(N, outs)[:, :L + 16].tobytes()).hexdigest())
 
@@ -55,13 +64,14 @@ def ref_digest(o, cfg):
     """C2's sealed digest through the reference's own CipherState API
     (oracle/_ref, built from /root/reference), one call per record."""
     ref = RefLib()
-    N, L = cfg["records"], cfg["len"]
+    N, L, AD = cfg["records"], cfg["len"], cfg.get("ad", 0)
     ins = stride(L)
     key = o.fill(SEED_KEY, 32, 0)
     pt = o.fill(SEED_PT, N * ins, 0)
+    ad = o.fill(SEED_AD, N * AD, 0) if AD else b""
     h = hashlib.sha256()
     for i in range(N):
-        h.update(ref.encrypt(cfg["cipher"], key, i, pt[i * ins:i * ins + L]))
+        h.update(ref.encrypt(cfg["cipher"], key, i, pt[i * ins:i * ins + L], ad[i * AD:(i + 1) * AD]))
     return h.hexdigest()
 
 
@@ -95,6 +105,22 @@ def c5_digest(o):
 def main():
     o = Oracle()
     out = {"generator": "tests/golden/gen_config_digests.py (CPU oracle)", "configs": {}}
+    only = sys.argv[1:]  # e.g. `perf`: add that config to the existing file, keep the others
+    path = os.path.join(ROOT, "tests", "golden", "config_digests.json")
+    if only:
+        with open(path) as f:
+            out = json.load(f)
+        for name in only:
+            t = time.time()
+            out["configs"][name] = digests(o, name, CONFIGS[name])
+            print(name, f"{time.time() - t:.1f}s", out["configs"][name]["sealed_sha256"][:16])
+            if os.path.exists(REF_SO) and CONFIGS[name]["states"] == 1:
+                assert ref_digest(o, CONFIGS[name]) == out["configs"][name]["sealed_sha256"], name
+                out["configs"][name]["reference_checked"] = True
+                print(name, "reference build agrees")
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return
     for name, cfg in CONFIGS.items():
         t = time.time()
         out["configs"][name] = digests(o, name, cfg)

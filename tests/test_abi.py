@@ -183,15 +183,15 @@ def test_batch_host_rules(aead_built):
 def test_default_lane_policy(aead_built):
     """Lanes per record the library picks (aead_api.hip uniform_lanes /
     auto_lanes): a standalone seal or open takes one lane per record from
-    128 Ki records (two waves per SIMD), two segments per record from 64 Ki
-    (chachapoly_seg.hip: two waves per SIMD again), 8 lanes below, and wide
+    128 Ki records (two waves per SIMD), 4 lanes from 64 Ki (two segments per
+    record measured slower there, aead_api.hip seg_mode), 8 below, and wide
     groups (up to a wave per record) only for batches of at most 512 records
     — the latency regime; the jobs of a duplex launch take one lane per
     record from 64 Ki records (the BASELINE sizes, FAST layouts)."""
     A = aead_built
     lanes = lambda n: A.dev_default_lanes(A.CHACHAPOLY, n)
     duplex = lambda n: A.dev_duplex_lanes(A.CHACHAPOLY, n)
-    assert lanes(65536) == 2 and lanes(131071) == 2 and lanes(131072) == 1 and lanes(1 << 20) == 1
+    assert lanes(65536) == 4 and lanes(131071) == 4 and lanes(131072) == 1 and lanes(1 << 20) == 1
     assert lanes(65535) == 8 and lanes(513) == 8
     assert lanes(512) == 64 and lanes(1) == 64
     assert duplex(65536) == 1 and duplex(1 << 20) == 1

@@ -163,7 +163,8 @@ def test_c5_shard_digest_on_gpu(rank):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,lanes,vf", [("c2", 0, False), ("c2", 4, False), ("c3", 0, False),
-                                           ("c2", 0, True), ("c3", 0, True)])
+                                           ("c2", 0, True), ("c3", 0, True), ("c4", 0, False),
+                                           ("perf", 0, False)])
 def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     """The kernels bench.py times: C2 / C3 at full size
     through noise_aead_dev_duplex_uniform at the bench's 128-B record slots
@@ -175,26 +176,42 @@ def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     sealed beforehand with 64 records tampered, accepts every other record
     with the plaintext digest and rejects (zeroes) exactly the tampered ones.
     vf: the open half with NOISE_AEAD_FLAG_VERIFY_FIRST (the bench's
-    --verify-first line, still one launch): rejected records never written."""
+    --verify-first line, still one launch): rejected records never written.
+    c4: the timed kernel of C4 — the one-lane duplex
+    over 4096 states x 256 records; perf: the duplex of 1024-B records with
+    32 B of AD each (both reference-checked digests, the perf one through
+    the reference's own CipherState API)."""
     import torch
 
     import noise_aead as A
     A.lib()
     c = _golden()[name]
-    N, L, cipher = c["records"], c["len"], c["cipher"]
-    ins, outs = 1408, 1536  # bench.py SLOT_ALIGN = 128
+    N, L, cipher, S, AD = c["records"], c["len"], c["cipher"], c["states"], c.get("ad", 0)
+    # bench.py SLOT_ALIGN = 128: strides roundup128(len), roundup128(len + 16)
+    ins, outs = (L + 127) // 128 * 128, (L + 16 + 127) // 128 * 128
+    # the golden plaintext is the SplitMix64 stream over 16-B slots
+    gins = c["in_stride"]
     sp = torch.cuda.current_stream().cuda_stream
-    raw = torch.empty(32, dtype=torch.uint8, device="cuda")
-    assert A.dev_fill_splitmix(raw.data_ptr(), 32, SEED_KEY, 0, sp) == 0
-    ctx = torch.empty(A.dev_ctx_bytes(cipher), dtype=torch.uint8, device="cuda")
-    assert A.dev_prepare(cipher, raw.data_ptr(), 1, ctx.data_ptr(), sp) == 0
-    nb = torch.zeros(1, dtype=torch.int64, device="cuda")
-    pt = torch.empty(N * ins, dtype=torch.uint8, device="cuda")
-    assert A.dev_fill_splitmix(pt.data_ptr(), pt.numel(), SEED_PT, 0, sp) == 0
+    raw = torch.empty(S * 32, dtype=torch.uint8, device="cuda")
+    for k in range(S):
+        assert A.dev_fill_splitmix(raw[32 * k:].data_ptr(), 32, SEED_KEY, 4 * k, sp) == 0
+    ctx = torch.empty(S * A.dev_ctx_bytes(cipher), dtype=torch.uint8, device="cuda")
+    assert A.dev_prepare(cipher, raw.data_ptr(), S, ctx.data_ptr(), sp) == 0
+    nb = torch.zeros(S, dtype=torch.int64, device="cuda")
+    gpt = torch.empty(N * gins, dtype=torch.uint8, device="cuda")
+    assert A.dev_fill_splitmix(gpt.data_ptr(), gpt.numel(), SEED_PT, 0, sp) == 0
+    pt = torch.zeros(N * ins, dtype=torch.uint8, device="cuda")
+    pt.view(N, ins)[:, :L] = gpt.view(N, gins)[:, :L]
+    del gpt
     assert hashlib.sha256(pt.view(N, ins)[:, :L].contiguous().cpu().numpy().tobytes()).hexdigest() \
         == c["pt_sha256"]
+    ad_kw = {}
+    if AD:
+        adb = torch.empty(N * AD, dtype=torch.uint8, device="cuda")
+        assert A.dev_fill_splitmix(adb.data_ptr(), adb.numel(), 0x6164, 0, sp) == 0
+        ad_kw = dict(ad=adb.data_ptr(), ad_stride=AD, ad_len=AD)
     common = dict(ctx=ctx.data_ptr(), nonce_base=nb.data_ptr(), length=L, n_records=N,
-                  recs_per_state=N, lanes=lanes)
+                  recs_per_state=N // S, lanes=lanes, **ad_kw)
     # batch B: sealed by the separate kernel, then tampered
     ct_b = torch.empty(N * outs, dtype=torch.uint8, device="cuda")
     assert A.dev_uniform(False, cipher, inp=pt.data_ptr(), out=ct_b.data_ptr(), in_stride=ins,

@@ -177,8 +177,9 @@ def test_uniform_seg2_vs_oracle(aead, gpu, oracle, vf, rps):
 
 
 def test_default_lanes_segmented(aead):
-    """The library's choice: two segments for a standalone 64 Ki-record
-    ChaChaPoly job, one lane from 128 Ki, one lane in a duplex launch."""
-    assert aead.dev_default_lanes(CHACHA, 65536) == 2
+    """The library's choice: four lanes for a standalone 64 Ki-record
+    ChaChaPoly job (two segments measured slower there), one lane from
+    128 Ki, one lane in a duplex launch."""
+    assert aead.dev_default_lanes(CHACHA, 65536) == 4
     assert aead.dev_default_lanes(CHACHA, 131072) == 1
     assert aead.dev_duplex_lanes(CHACHA, 65536) == 1
