@@ -1089,7 +1089,10 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     alg = 2 * g["bytes"] + 16 * g["n"] + 40 * g["states"]
     achieved = alg / (ms * 1e-3) / 1e9
     # the kernel the library dispatches (aead_api.hip run_ragged), as rocprofv3 names it
-    if g["cipher"] == CHACHA:  # run_ragged: 8 lanes below 128 Ki records, else 4
+    if g["cipher"] == CHACHA and not args.lanes and os.environ.get("NOISE_AEAD_SEG", "1") != "0" \
+            and g["n"] >= 16384:  # run_ragged: the segmented one-lane kernel (chachapoly_seg.hip)
+        kname = f"chachapoly_seg_ragged<{'true' if open_ else 'false'}>"
+    elif g["cipher"] == CHACHA:  # run_ragged: 8 lanes below 128 Ki records, else 4
         k = args.lanes or (8 if g["n"] < 131072 else 4)
         kname = (f"chachapoly_open_ragged<{k}, true, {'true' if args.verify_first else 'false'}>"
                  if open_ else f"chachapoly_seal_ragged<{k}, true>")

@@ -415,9 +415,21 @@ int noise_aead_debug_worker_placement(void);
  *   the host, ns from its start: packed, doorbell, done seen, returned. */
 void noise_aead_debug_worker_host_ns(uint64_t *out, int n);
 void *noise_aead_debug_last_freed_ctx(size_t *bytes);
-/* noise_aead_debug_workers_resident: resident single-call workers of the
- *   current device whose kernel is still running (-1: no device). */
+/* noise_aead_debug_workers_resident: request slots (one workgroup each) of
+ *   the current device whose worker group is still running (-1: no device). */
 int noise_aead_debug_workers_resident(void);
+/* noise_aead_debug_worker_launches: worker group kernels launched on the
+ *   current device so far. */
+unsigned noise_aead_debug_worker_launches(void);
+/* noise_aead_debug_worker_group_launches: out[g] = launches of group g
+ *   (g < 8), out[8..11] = the relaunch checks by cause (not launched,
+ *   slot exiting at the call, slot exiting while waiting, no launch needed). */
+void noise_aead_debug_worker_group_launches(unsigned *out, int n);
+/* noise_aead_debug_worker_leave_reason / _leave_info: why slot `slot` of
+ *   group `group` last left (1 stop, 2 another slot closed the group, 4 idle,
+ *   8 lifetime) and its born / leave times (10-ns ticks), lifetime, launch. */
+unsigned noise_aead_debug_worker_leave_reason(int group, int slot);
+void noise_aead_debug_worker_leave_info(int group, int slot, unsigned *out);
 
 /* Default lanes per record the library picks for a standalone uniform seal
  * or open of n records (noise_aead_dev_{seal,open}_uniform, lanes 0) in a

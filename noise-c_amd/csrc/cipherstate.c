@@ -119,6 +119,73 @@ Staging *na_stage_get(size_t bytes)
 
 /* --------------------------------------------------- device key contexts */
 
+/* Key-context memory is recycled, never handed back to HIP while the
+   library runs: hipFree / hipHostFree wait for every stream of the device,
+   and a resident worker group (worker.hip) ends only after 2 ms without
+   calls, up to its 5 s lifetime while calls keep coming — freeing one state
+   used to stall for seconds beside another thread's single calls.  A
+   released context is scrubbed first (device: zeroed and waited for; host
+   copy: na_clean) and then kept on a free list per device, kind and size;
+   the lists hold at most the peak number of live states' contexts. */
+typedef struct CtxBuf {
+    void *p;
+    size_t bytes;
+    int device, host;
+    struct CtxBuf *next;
+} CtxBuf;
+static CtxBuf *g_ctx_free;
+static pthread_mutex_t g_ctx_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static void *ctx_take(int device, int host, size_t bytes)
+{
+    pthread_mutex_lock(&g_ctx_mu);
+    for (CtxBuf **pp = &g_ctx_free; *pp; pp = &(*pp)->next) {
+        CtxBuf *b = *pp;
+        if (b->device == device && b->host == host && b->bytes == bytes) {
+            *pp = b->next;
+            pthread_mutex_unlock(&g_ctx_mu);
+            void *p = b->p;
+            free(b);
+            return p;
+        }
+    }
+    pthread_mutex_unlock(&g_ctx_mu);
+    return NULL;
+}
+
+/* p already scrubbed; if the list node cannot be had, the memory is freed
+   (and that free may wait for the device, as before) */
+static void ctx_give(void *p, int device, int host, size_t bytes)
+{
+    CtxBuf *b = (CtxBuf *)malloc(sizeof(CtxBuf));
+    if (!b) {
+        if (host) (void)hipHostFree(p);
+        else (void)hipFree(p);
+        return;
+    }
+    b->p = p;
+    b->bytes = bytes;
+    b->device = device;
+    b->host = host;
+    pthread_mutex_lock(&g_ctx_mu);
+    b->next = g_ctx_free;
+    g_ctx_free = b;
+    pthread_mutex_unlock(&g_ctx_mu);
+}
+
+/* (worker_crypt) the pinned host copy of an AES-GCM context */
+static int h_ctx_alloc(HipCipherState *st, size_t bytes)
+{
+    st->h_ctx = ctx_take(-1, 1, bytes);
+    if (st->h_ctx) return 0;
+    if (hipHostMalloc((void **)&st->h_ctx, bytes, hipHostMallocMapped | hipHostMallocCoherent |
+                                                   hipHostMallocPortable) != hipSuccess) {
+        st->h_ctx = NULL;
+        return -1;
+    }
+    return 0;
+}
+
 
 /* Zero n bytes of device memory on `device` and wait for it, so that key
    material is gone before the allocation can be handed out again
@@ -149,8 +216,9 @@ static void release_ctx(HipCipherState *st)
 {
     if (st->h_ctx) { /* the worker's pinned copy holds key material too */
         na_worker_forget_ctx(st->h_ctx); /* and so may a worker's LDS cache of it */
-        na_clean(st->h_ctx, noise_aead_dev_ctx_bytes(st->parent.cipher_id));
-        (void)hipHostFree(st->h_ctx);
+        const size_t hb = noise_aead_dev_ctx_bytes(st->parent.cipher_id);
+        na_clean(st->h_ctx, hb);
+        ctx_give(st->h_ctx, -1, 1, hb);
         st->h_ctx = NULL;
         st->h_ctx_ready = 0;
     }
@@ -162,11 +230,7 @@ static void release_ctx(HipCipherState *st)
         g_dbg_freed_ctx = st->d_ctx;
         g_dbg_freed_bytes = bytes;
     } else {
-        int cur = 0;
-        (void)hipGetDevice(&cur);
-        if (cur != st->device) (void)hipSetDevice(st->device);
-        (void)hipFree(st->d_ctx);
-        if (cur != st->device) (void)hipSetDevice(cur);
+        ctx_give(st->d_ctx, st->device, 0, bytes);
     }
     st->d_ctx = NULL;
     st->ctx_ready = 0;
@@ -184,7 +248,8 @@ int na_ensure_ctx(HipCipherState *st, Staging *sg)
     st->ctx_ready = 0;
     if (!st->d_ctx) {
         size_t bytes = noise_aead_dev_ctx_bytes(st->parent.cipher_id);
-        if (hipMalloc(&st->d_ctx, bytes) != hipSuccess) {
+        st->d_ctx = ctx_take(dev, 0, bytes);
+        if (!st->d_ctx && hipMalloc(&st->d_ctx, bytes) != hipSuccess) {
             st->d_ctx = NULL;
             return NOISE_ERROR_SYSTEM;
         }
@@ -561,12 +626,7 @@ static int worker_crypt(HipCipherState *st, const uint8_t *ad, size_t ad_len, ui
             const size_t bytes = noise_aead_dev_ctx_bytes(NOISE_CIPHER_AESGCM);
             Staging *sg = na_stage_get(64);
             if (!sg || na_ensure_ctx(st, sg)) return NOISE_ERROR_NOT_APPLICABLE;
-            if (!st->h_ctx && hipHostMalloc((void **)&st->h_ctx, bytes,
-                                            hipHostMallocMapped | hipHostMallocCoherent |
-                                            hipHostMallocPortable) != hipSuccess) {
-                st->h_ctx = NULL;
-                return NOISE_ERROR_NOT_APPLICABLE;
-            }
+            if (!st->h_ctx && h_ctx_alloc(st, bytes)) return NOISE_ERROR_NOT_APPLICABLE;
             if (hipMemcpy(st->h_ctx, st->d_ctx, bytes, hipMemcpyDeviceToHost) != hipSuccess)
                 return NOISE_ERROR_NOT_APPLICABLE;
             /* a new generation: the worker's cached copy of this address is stale */

@@ -28,12 +28,18 @@
  * thread of the workgroup (one barrier-synchronised loop).  Before leaving it
  * sets `exiting` and looks at seq once more, so a request posted meanwhile
  * is either served or seen by the host (exiting set, done behind): the host
- * then waits for the stream and starts a new worker at the same seq.  A
- * device runs up to workers_per_dev() workers (one per high-priority
- * hardware queue: 4 by default), each with its own slot and stream: a
- * calling thread takes a free one without waiting (its own first), so N
- * threads on N CipherStates make up to that many calls at once.  Batch
- * launches that fill every CU ask the resident workers to leave first
+ * then waits for the stream and starts the worker again, which resumes at
+ * the slot's `done`.
+ *
+ * Workers come in GROUPS: one kernel of S workgroups (request slots) on one
+ * high-priority stream, so S calling threads share a hardware queue (a queue
+ * runs nothing else while a resident kernel holds it).  A device runs one
+ * group per high-priority queue but one (3 by default, the last left to the
+ * application), S = ceil(8 / groups) slots each: 9 slots, one per calling
+ * thread up to 9, each a workgroup on its own CU, claimed without waiting
+ * while one is free.  A group leaves as a whole (aead_worker: the closing
+ * word), for idleness only once all its slots are idle.  Batch launches that
+ * fill every CU ask the resident groups to leave first
  * (worker_park_for_batch), so no batch workgroup waits for a worker's CU.
  *
  * Key material reaches the worker through the slot as well: the ChaCha key
@@ -113,7 +119,8 @@ struct alignas(128) WorkerSlot {
     uint32_t exiting;  /* the worker is leaving (or has left) */
     uint32_t stamps[8]; /* debug: s_memrealtime (10 ns) of the last request's phases */
     uint32_t fstamps[8]; /* debug: s_memtime (cycles) through the latency-first path */
-    uint8_t pad1[128 - 80];
+    uint32_t leave[4];   /* debug: the last leave's born, now (10 ns ticks, low words), lifetime, gen */
+    uint8_t pad1[128 - 96];
 };
 static_assert(sizeof(WorkerSlot) == 256, "slot layout");
 
@@ -521,14 +528,50 @@ NA_DEV uint4 load_sys16_raw(const uint8_t *p)
 #endif
 constexpr uint64_t POLL_BACKOFF = NA_POLL_BACKOFF;
 
-/* 256 threads.  req: the header chunks (4 in host memory; 8 in device
-   memory, vram); in: the stream's stamped chunks, tail: the rest raw; last:
-   the last request already served; idle/lifetime in s_memrealtime ticks
-   (100 MHz). */
-__global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint32_t *req, const uint4 *in,
-                                                   uint32_t vram, const uint8_t *tail, uint8_t *out,
-                                                   uint32_t last, uint64_t idle, uint64_t lifetime)
+/* A worker GROUP is one kernel of nslots workgroups on one high-priority
+   stream, workgroup i serving request slot i: several calling threads per
+   hardware queue (4 queues served at most 4 threads).  A group
+   ends as a whole — a hardware queue runs nothing else until its kernel has
+   left — so the workgroups agree on leaving through the group words (in the
+   slots' placement, polled with the header in the same load instruction):
+   word 0 `closing`, set by the first workgroup to leave (stop, idle,
+   lifetime), after which every workgroup leaves between requests; words
+   1..nslots the workgroups' last-request times.  A workgroup leaves for
+   idleness only when every slot of the group has been idle that long.  Only
+   the device writes the group words (`closing` is the number of the launch
+   that closed, never reset by the host). */
+constexpr int WORKER_MAX_SLOTS = 4;
+struct WorkerSlotArgs {
+    WorkerSlot *slot;      /* device view of the slot */
+    const uint32_t *req;   /* the header chunks (4 in host memory; 8 in device memory, vram) */
+    const uint4 *in;       /* the stream's stamped chunks */
+    const uint8_t *tail;   /* the rest of the stream, raw */
+    uint8_t *out;          /* results */
+    uint32_t vram;
+    uint32_t pad_;
+};
+struct WorkerArgs {
+    WorkerSlotArgs s[WORKER_MAX_SLOTS];
+    uint32_t *group;       /* the group words (8) */
+    uint32_t nslots;
+    uint32_t gen;          /* this launch's number: `closing` holds the number of the launch that closed */
+    uint64_t idle, lifetime; /* s_memrealtime ticks (100 MHz) */
+};
+
+/* 256 threads per workgroup, one workgroup per slot. */
+__global__ __launch_bounds__(256) void aead_worker(WorkerArgs a)
 {
+    const uint32_t me = blockIdx.x;
+    WorkerSlot *const slot = a.s[me].slot;
+    const uint32_t *const req = a.s[me].req;
+    const uint4 *const in = a.s[me].in;
+    const uint8_t *const tail = a.s[me].tail;
+    uint8_t *const out = a.s[me].out;
+    const uint32_t vram = a.s[me].vram;
+    const uint64_t idle = a.idle, lifetime = a.lifetime;
+    /* the last request served on this slot (a relaunched group starts where
+       the one before it stopped: a request it left unserved is served) */
+    uint32_t last = (uint32_t)NA_SYS_LOAD(&slot->done);
     const uint32_t head = vram ? VWORKER_HEAD : WORKER_HEAD, cbytes = vram ? VCHUNK_BYTES : WCHUNK_BYTES;
     __shared__ uint32_t te[256], sb[256];
     __shared__ __attribute__((aligned(16))) uint8_t cbuf[WORKER_CTX_SLOTS][WORKER_CTX_BYTES];
@@ -549,6 +592,12 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
     }
     const uint64_t born = __builtin_amdgcn_s_memrealtime();
     uint64_t quiet = born;
+    /* the group word of this slot's last-request time is refreshed at most
+       every idle / 8 (a system store the next poll would wait for: +0.7 us
+       per call when written after every request); the idle test allows for
+       the lag */
+    uint64_t stamped = born;
+    if (t == 0) NA_SYS_STORE(&a.group[1 + me], (uint32_t)born);
     bool leaving = false;
     uint32_t tick = 0;
     __shared__ uint32_t s_slow; /* backed-off polling (see below) */
@@ -564,8 +613,10 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
            request then re-reads its chunks once (stamp 0 is never current).
            A wave may see the previous poll's setting: both are correct. */
         uint4 c = make_uint4(0, 0, 0, 0), mine = make_uint4(0, 0, 0, 0);
-        if (!s_slow) load_sys16x2(req + 4 * (t & (vram ? 15 : 7)), (const uint32_t *)(in + t), c, mine);
-        else if (t < 64) c = load_sys16(req + 4 * (t & (vram ? 15 : 7)));
+        /* lanes 14 and 15 of every 16 read the group words instead */
+        const uint32_t *hp = (t & 15) >= 14 ? a.group + 4 * (t & 1) : req + 4 * (t & (vram ? 15 : 7));
+        if (!s_slow) load_sys16x2(hp, (const uint32_t *)(in + t), c, mine);
+        else if (t < 64) c = load_sys16(hp);
         if (t == 0) s_stale = 0;
         if (t < 64) {
             const uint32_t s0 = __shfl((int)c.x, 0, 64);
@@ -591,17 +642,35 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
                     }
                 }
             }
+            /* the group words: closing, then the slots' last-request times */
+            const bool closing = (uint32_t)__shfl((int)c.x, 14, 64) == a.gen;
+            const uint32_t gq[WORKER_MAX_SLOTS] = {(uint32_t)__shfl((int)c.y, 14, 64),
+                                                   (uint32_t)__shfl((int)c.z, 14, 64),
+                                                   (uint32_t)__shfl((int)c.w, 14, 64),
+                                                   (uint32_t)__shfl((int)c.x, 15, 64)};
             if (t == 0) {
                 uint32_t cmd = 0;
                 const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                bool group_idle = now - quiet > idle;
+                for (uint32_t j = 0; j < a.nslots; ++j) /* 32-bit tick differences: idle < 2^31 */
+                    if ((uint32_t)now - gq[j] <= (uint32_t)(idle + idle / 8)) group_idle = false;
                 if (fresh) {
                     cmd = 1;
                 } else if (leaving) {
                     cmd = 2;
-                } else if (stop || now - quiet > idle || now - born > lifetime) {
-                    /* announce, then poll once more: a request posted before
-                       that poll is served; one posted after it finds
-                       `exiting` set and the host starts a new worker */
+                } else if (stop || closing || group_idle || now - born > lifetime) {
+                    /* the group leaves with this workgroup; announce, then
+                       poll once more: a request posted before that poll is
+                       served; one posted after it finds `exiting` set and the
+                       host starts the group again once all of it has left */
+                    /* debug: why (stamps[7]: 1 stop, 2 closing, 4 idle, 8 lifetime) */
+                    slot->stamps[7] = (stop ? 1u : 0u) | (closing ? 2u : 0u) | (group_idle ? 4u : 0u) |
+                                      (now - born > lifetime ? 8u : 0u);
+                    slot->leave[0] = (uint32_t)born;
+                    slot->leave[1] = (uint32_t)now;
+                    slot->leave[2] = (uint32_t)lifetime;
+                    slot->leave[3] = a.gen;
+                    NA_SYS_STORE(&a.group[0], a.gen);
                     NA_SYS_STORE(&slot->exiting, 1u);
                     leaving = true;
                 } else if (now - quiet > POLL_BACKOFF) {
@@ -719,6 +788,10 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
         }
         last = seq;
         quiet = __builtin_amdgcn_s_memrealtime();
+        if (quiet - stamped > idle / 8) {
+            if (t == 0) NA_SYS_STORE(&a.group[1 + me], (uint32_t)quiet);
+            stamped = quiet;
+        }
         /* scrub this record's bytes (and the key) from LDS before the next one;
            the kernels may have written whole 64-B units past len + 16 */
         for (uint32_t o = 16 * t; o < bytes + 64; o += 16 * 256) *(uint4 *)(buf + o) = make_uint4(0, 0, 0, 0);
@@ -733,11 +806,12 @@ __global__ __launch_bounds__(256) void aead_worker(WorkerSlot *slot, const uint3
 
 namespace {
 
+struct WorkerGroup;
+
+/* One request slot: served by one workgroup of its group's kernel. */
 struct Worker {
-    std::mutex mu;
-    int state = 0;             /* 0 unknown, 1 usable, -1 disabled, -2 draining (worker_abandon) */
-    uint32_t launches = 0;     /* debug: kernels launched (noise_aead_debug_worker_launches) */
-    int launch_fails = 0;      /* consecutive failed launches (3 disable the worker) */
+    std::mutex mu;             /* held by the calling thread for a whole call */
+    int state = 0;             /* 0 not set up, 1 usable, -1 failed */
     WorkerSlot *slot = nullptr; /* host view */
     WorkerSlot *dslot = nullptr; /* device view */
     /* the request (header chunks, stream): in fine-grained device memory the
@@ -749,36 +823,49 @@ struct Worker {
     uint4 *in = nullptr, *din = nullptr;       /* the stream's head: stamped chunks */
     uint8_t *tail = nullptr, *dtail = nullptr; /* the rest of the stream, raw */
     uint8_t *out = nullptr, *dout = nullptr;   /* raw results */
-    hipStream_t stream = nullptr;
     uint32_t seq = 0;
-    bool launched = false;     /* written under mu, read by park() with atomics */
-    /* the AES-GCM contexts (host copies) sent to the running worker, whose
-       LDS cache may hold them: only a worker that was sent a context is
-       parked when the state is freed; past kCtxHist distinct
-       ones since its launch, any free parks it */
+    /* the AES-GCM contexts (host copies) sent to this slot's workgroup, whose
+       LDS cache may hold them: only a group one of whose slots was sent a
+       context is parked when the state is freed; past kCtxHist
+       distinct ones since the group's launch, any free parks it */
     static constexpr int kCtxHist = 8;
     const void *ctx_hist[kCtxHist] = {};
-    uint32_t ctx_n = 0;        /* written under mu, read by forget() with atomics */
+    uint32_t ctx_n = 0;        /* written under mu (or at launch), read by forget() with atomics */
+    WorkerGroup *g = nullptr;
+};
+
+/* One kernel on one high-priority stream: nslots workgroups, one per slot. */
+struct WorkerGroup {
+    std::mutex mu;             /* launch, drain, recover (taken after a slot's mu, never before) */
+    int state = 0;             /* 0 unknown, 1 usable, -1 disabled, -2 draining (worker_abandon) */
+    uint32_t launches = 0;     /* debug: kernels launched (noise_aead_debug_worker_launches) */
+    int launch_fails = 0;      /* consecutive failed launches (3 disable the group) */
+    hipStream_t stream = nullptr;
+    bool launched = false;     /* written under mu, read by park() with atomics */
+    uint32_t gen = 0;          /* launches so far (atomics): a relaunch happens once */
+    uint32_t abandoned = 0;    /* slots whose request was abandoned: results scrubbed on recovery */
+    uint32_t *words = nullptr; /* host view of the group words (8) */
+    uint32_t *dwords = nullptr;
+    bool words_vram = false;
+    int nslots = 1;
+    Worker slot[WORKER_MAX_SLOTS];
 };
 
 constexpr int kMaxDev = 64;
-/* Resident workers a device may run at once.  A CipherState is single-owner
-   with no locks (cipherstate.c:293-410), so N threads calling on N states
-   run N calls at once on the CPU; here each calling thread gets a worker of
-   its own (a workgroup on its own CU, launched on first use and gone 2 ms
-   after its last request), claimed without waiting while one is free. */
-constexpr int kWorkersPerDev = 8;
+constexpr int kMaxGroups = 8;
 
-/* A resident worker never ends while calls keep coming (up to LIFETIME), so
+/* A resident group never ends while calls keep coming (up to LIFETIME), so
    it must own its hardware queue: a kernel queued behind it on the same AQL
    queue waits for it to leave.  HIP maps streams onto GPU_MAX_HW_QUEUES
-   queues per device and priority (4 by default), so the workers run on
+   queues per device and priority (4 by default), so the groups run on
    high-priority streams — a pool apart from the application's normal
    streams (tools/queue_probe.cpp: a memset on a new normal stream waited
    the worker's whole 5 s lifetime beside a normal-priority worker, 20-60 us
-   beside high-priority ones) — and a device runs at most as many workers
-   as that pool has queues, so no two workers share one.  More concurrent
-   workers: raise GPU_MAX_HW_QUEUES (up to kWorkersPerDev are used).
+   beside high-priority ones) — and a device runs one group per queue of that
+   pool but one: the last queue stays free for a high-priority stream of the
+   application's own.  NOISE_AEAD_WORKER_QUEUES sets the number
+   of queues the groups take instead (1..8; an application with several
+   high-priority streams of its own lowers it, or raises GPU_MAX_HW_QUEUES).
    NOISE_AEAD_WORKER_PRIO=normal / low: the A/B placements. */
 int worker_stream_prio()
 {
@@ -790,20 +877,42 @@ int worker_stream_prio()
     return v;
 }
 
-int workers_per_dev()
+int hw_queues()
+{
+    const char *e = getenv("GPU_MAX_HW_QUEUES");
+    const int q = e ? atoi(e) : 4;
+    return q < 1 ? 4 : q;
+}
+
+int groups_per_dev()
 {
     static const int v = [] {
-        const char *e = getenv("GPU_MAX_HW_QUEUES");
-        int q = e ? atoi(e) : 4;
-        if (q < 1) q = 4;
-        return q < kWorkersPerDev ? q : kWorkersPerDev;
+        const char *e = getenv("NOISE_AEAD_WORKER_QUEUES");
+        int g = e && atoi(e) > 0 ? atoi(e) : (hw_queues() > 1 ? hw_queues() - 1 : 1);
+        return g < kMaxGroups ? g : kMaxGroups;
     }();
     return v;
 }
-Worker g_worker[kMaxDev][kWorkersPerDev];
+
+/* Slots per group: enough for 8 calling threads over the groups
+   (NOISE_AEAD_WORKER_SLOTS: 1..4).  A CipherState is single-owner with no
+   locks (cipherstate.c:293-410), so N threads on N states run N calls at once
+   on the CPU; here each calling thread gets a slot of its own (a workgroup on
+   its own CU), claimed without waiting while one is free. */
+int slots_per_group()
+{
+    static const int v = [] {
+        const char *e = getenv("NOISE_AEAD_WORKER_SLOTS");
+        int s = e && atoi(e) > 0 ? atoi(e) : (8 + groups_per_dev() - 1) / groups_per_dev();
+        return s < WORKER_MAX_SLOTS ? s : WORKER_MAX_SLOTS;
+    }();
+    return v;
+}
+
+WorkerGroup g_group[kMaxDev][kMaxGroups];
 std::atomic<uint32_t> g_next_pref{0};
-thread_local int t_pref = -1;             /* this thread's first-choice worker */
-thread_local Worker *t_last = nullptr;    /* the worker of this thread's last call (debug hooks) */
+thread_local int t_pref = -1;             /* this thread's first-choice slot (spread over groups first) */
+thread_local Worker *t_last = nullptr;    /* the slot of this thread's last call (debug hooks) */
 std::once_flag g_atexit_once;
 
 constexpr uint64_t IDLE_TICKS = 200000;       /* 2 ms at 100 MHz */
@@ -817,9 +926,9 @@ uint64_t idle_ticks()
     return v;
 }
 constexpr uint64_t LIFETIME_TICKS = 500000000; /* 5 s */
-/* The longest request (a 65519-B AES-GCM record) takes ~0.4 ms; a worker
+/* The longest request (a 65519-B AES-GCM record) takes ~0.4 ms; a group
    that has not answered after this is taken for lost: the call falls back to
-   the launch path and the worker is not used again. */
+   the launch path and the group is drained before it is used again. */
 constexpr uint64_t WAIT_LIMIT_NS = 2000000000ull; /* 2 s */
 
 /* the stop word: chunk 4 of the host slot, chunk 8 of the device request
@@ -827,25 +936,29 @@ constexpr uint64_t WAIT_LIMIT_NS = 2000000000ull; /* 2 s */
    rewrite */
 uint32_t *stop_word(Worker &w) { return w.vram ? &w.req[4 * 8] : &w.req[4 * 4]; }
 
-/* Ask a launched worker to leave (no wait).  A worker leaving scrubs its
-   LDS; a request racing with the stop is either served or seen by its
-   caller as `exiting` (the caller then starts a new worker).  The stop word
-   has a chunk of its own, so no request header written meanwhile can undo
-   it. */
-void park_worker(Worker &w)
+void set_stops(WorkerGroup &g, uint32_t v)
 {
-    if (__atomic_load_n(&w.launched, __ATOMIC_ACQUIRE)) {
-        __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
-        _mm_sfence();
-    }
+    for (int i = 0; i < g.nslots; ++i)
+        if (g.slot[i].state == 1) __atomic_store_n(stop_word(g.slot[i]), v, __ATOMIC_RELEASE);
+    _mm_sfence();
+}
+
+/* Ask a launched group to leave (no wait).  A workgroup leaving scrubs its
+   LDS; a request racing with the stop is either served or seen by its caller
+   as `exiting` (the caller then starts the group again).  The stop words
+   have chunks of their own, so no request header written meanwhile can undo
+   them. */
+void park_group(WorkerGroup &g)
+{
+    if (__atomic_load_n(&g.launched, __ATOMIC_ACQUIRE)) set_stops(g, 1u);
 }
 
 void park_device(int dev)
 {
-    for (int i = 0; i < kWorkersPerDev; ++i) park_worker(g_worker[dev][i]);
+    for (int i = 0; i < kMaxGroups; ++i) park_group(g_group[dev][i]);
 }
 
-/* Did worker w (maybe) receive AES-GCM context h since its launch? */
+/* Did slot w (maybe) receive AES-GCM context h since its group's launch? */
 bool worker_saw_ctx(const Worker &w, const void *h)
 {
     const uint32_t n = __atomic_load_n(&w.ctx_n, __ATOMIC_ACQUIRE);
@@ -855,7 +968,7 @@ bool worker_saw_ctx(const Worker &w, const void *h)
     return false;
 }
 
-/* (under w.mu) record that context h goes to worker w */
+/* (under w.mu) record that context h goes to slot w */
 void worker_note_ctx(Worker &w, const void *h)
 {
     const uint32_t n = w.ctx_n;
@@ -866,44 +979,49 @@ void worker_note_ctx(Worker &w, const void *h)
     __atomic_store_n(&w.ctx_n, n + 1, __ATOMIC_RELEASE);
 }
 
-/* A request the worker did not answer within WAIT_LIMIT_NS (under w.mu):
-   the worker is asked to leave and the request's header is made
-   unservable — its first chunk no longer agrees with the others — so a late
-   worker cannot take it; the worker is drained (state -2) and made usable
-   again once its stream is idle (worker_recover), when its result area is
-   scrubbed once more in case a late worker wrote it. */
+/* A request the group did not answer within WAIT_LIMIT_NS (under w.mu): the
+   group is asked to leave and the request's header is made unservable — its
+   first chunk no longer agrees with the others — so a late workgroup cannot
+   take it; the group is drained (state -2) and made usable again once its
+   stream is idle (worker_recover), when the slot's result area is scrubbed
+   once more in case a late workgroup wrote it. */
 void worker_abandon(Worker &w, uint32_t k)
 {
-    __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
+    WorkerGroup &g = *w.g;
+    std::lock_guard<std::mutex> gl(g.mu);
+    set_stops(g, 1u);
     const uint32_t bad = k ^ 0x80000000u;
     const __m128i c = w.vram ? _mm_set_epi32(0, (int)bad, 0, (int)bad) : _mm_set_epi32(0, 0, 0, (int)bad);
     _mm_store_si128((__m128i *)w.req, c);
     _mm_sfence();
-    w.state = -2;
+    g.abandoned |= 1u << (int)(&w - g.slot);
+    g.state = -2;
 }
 
-/* (under w.mu) a drained worker whose stream has gone idle: results
-   scrubbed, usable again (relaunched by the next call) */
-void worker_recover(Worker &w)
+/* (under g.mu) a drained group whose stream has gone idle: the abandoned
+   slots' results scrubbed, usable again (relaunched by the next call) */
+void worker_recover(WorkerGroup &g)
 {
-    if (w.state != -2 || hipStreamQuery(w.stream) != hipSuccess) return;
-    explicit_bzero(w.out, WORKER_DATA);
-    __atomic_store_n(&w.launched, false, __ATOMIC_RELEASE);
-    w.state = 1;
+    if (g.state != -2 || hipStreamQuery(g.stream) != hipSuccess) return;
+    for (int i = 0; i < g.nslots; ++i)
+        if (g.abandoned & (1u << i)) explicit_bzero(g.slot[i].out, WORKER_DATA);
+    g.abandoned = 0;
+    __atomic_store_n(&g.launched, false, __ATOMIC_RELEASE);
+    g.state = 1;
 }
 
 void worker_stop_all()
 {
     for (int d = 0; d < kMaxDev; ++d)
-        for (int i = 0; i < kWorkersPerDev; ++i) {
-            Worker &w = g_worker[d][i];
-            std::lock_guard<std::mutex> lk(w.mu);
-            if ((w.state != 1 && w.state != -2) || !w.launched) continue;
-            __atomic_store_n(stop_word(w), 1u, __ATOMIC_RELEASE);
-            _mm_sfence();
-            (void)hipStreamSynchronize(w.stream);
-            if (w.state == -2) explicit_bzero(w.out, WORKER_DATA); /* a late worker's results */
-            __atomic_store_n(&w.launched, false, __ATOMIC_RELEASE);
+        for (int i = 0; i < kMaxGroups; ++i) {
+            WorkerGroup &g = g_group[d][i];
+            std::lock_guard<std::mutex> lk(g.mu);
+            if ((g.state != 1 && g.state != -2) || !g.launched) continue;
+            set_stops(g, 1u);
+            (void)hipStreamSynchronize(g.stream);
+            for (int s = 0; s < g.nslots; ++s) /* a late workgroup's results */
+                if (g.abandoned & (1u << s)) explicit_bzero(g.slot[s].out, WORKER_DATA);
+            __atomic_store_n(&g.launched, false, __ATOMIC_RELEASE);
         }
 }
 
@@ -930,7 +1048,7 @@ bool vram_wanted(int dev)
     return hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) == hipSuccess && large_bar;
 }
 
-int worker_setup(Worker &w, int dev)
+int slot_setup(Worker &w, int dev)
 {
     if (w.state) return w.state;
     w.state = -1;
@@ -960,22 +1078,48 @@ int worker_setup(Worker &w, int dev)
         w.in = w.din = (uint4 *)((uint8_t *)w.vbase + 256);
         w.tail = w.dtail = (uint8_t *)(w.in + WORKER_SPEC);
     }
-    if (worker_stream_prio() == 0) {
-        if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess) return -1;
-    } else {
-        int least = 0, greatest = 0;
-        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return -1;
-        if (hipStreamCreateWithPriority(&w.stream, hipStreamNonBlocking,
-                                        worker_stream_prio() > 0 ? greatest : least) != hipSuccess)
-            return -1;
-    }
-    std::call_once(g_atexit_once, [] { atexit(worker_stop_all); });
     w.state = 1;
     return 1;
 }
 
+/* (under g.mu) the group's stream, words and slots, once */
+int group_setup(WorkerGroup &g, int dev)
+{
+    if (g.state) return g.state;
+    g.state = -1;
+    g.nslots = slots_per_group();
+    for (int i = 0; i < g.nslots; ++i) {
+        g.slot[i].g = &g;
+        if (slot_setup(g.slot[i], dev) != 1) return -1;
+    }
+    void *vw = nullptr;
+    if (g.slot[0].vram && hipExtMallocWithFlags(&vw, 256, hipDeviceMallocFinegrained) == hipSuccess) {
+        memset(vw, 0, 256);
+        _mm_sfence();
+        g.words = g.dwords = (uint32_t *)vw;
+        g.words_vram = true;
+    } else {
+        if (hipHostMalloc((void **)&g.words, 256, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return -1;
+        memset(g.words, 0, 256);
+        if (hipHostGetDevicePointer((void **)&g.dwords, g.words, 0) != hipSuccess) return -1;
+    }
+    if (worker_stream_prio() == 0) {
+        if (hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking) != hipSuccess) return -1;
+    } else {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return -1;
+        if (hipStreamCreateWithPriority(&g.stream, hipStreamNonBlocking,
+                                        worker_stream_prio() > 0 ? greatest : least) != hipSuccess)
+            return -1;
+    }
+    std::call_once(g_atexit_once, [] { atexit(worker_stop_all); });
+    g.state = 1;
+    return 1;
+}
+
 /* NOISE_ERROR_NONE, or NOISE_ERROR_NOT_APPLICABLE (the caller takes the
-   launch path; three failures in a row retire the worker) */
+   launch path; three failures in a row retire the group) */
 /* Test hook: NOISE_AEAD_DEBUG_WORKER_FAIL=1 makes every worker launch fail
    (tests/test_gpu_worker.py: the calls must then take the launch path). */
 bool debug_launch_fails()
@@ -998,53 +1142,114 @@ bool park_enabled()
     return v;
 }
 
-int worker_launch(Worker &w)
+/* (under g.mu, by the caller of slot `own`, whose mu it holds) start the
+   group once the kernel before it has left: every slot's exiting and stop
+   cleared, the closing word cleared.  Each workgroup starts at its slot's
+   `done`, so a request a leaving group did not take is served now. */
+int group_launch(WorkerGroup &g, Worker &own)
 {
-    (void)hipStreamSynchronize(w.stream); /* a previous worker has left */
+    (void)hipStreamSynchronize(g.stream); /* the kernel before has left (all its workgroups) */
     if (debug_launch_fails()) {
-        if (++w.launch_fails >= 3) w.state = -1;
+        if (++g.launch_fails >= 3) g.state = -1;
         return NOISE_ERROR_NOT_APPLICABLE;
     }
-    __atomic_store_n(&w.slot->exiting, 0u, __ATOMIC_RELEASE);
-    __atomic_store_n(stop_word(w), 0u, __ATOMIC_RELEASE);
+    WorkerArgs a = {};
+    for (int i = 0; i < g.nslots; ++i) {
+        Worker &w = g.slot[i];
+        __atomic_store_n(&w.slot->exiting, 0u, __ATOMIC_RELEASE);
+        __atomic_store_n(stop_word(w), 0u, __ATOMIC_RELEASE);
+        /* a fresh group caches nothing: the history restarts for slots not
+           in a call (a slot in a call may be noting a context right now) */
+        if (&w == &own) {
+            __atomic_store_n(&w.ctx_n, 0u, __ATOMIC_RELEASE);
+        } else {
+            std::unique_lock<std::mutex> l(w.mu, std::try_to_lock);
+            if (l.owns_lock()) __atomic_store_n(&w.ctx_n, 0u, __ATOMIC_RELEASE);
+        }
+        a.s[i].slot = w.dslot;
+        a.s[i].req = w.dreq;
+        a.s[i].in = (const uint4 *)w.din;
+        a.s[i].tail = (const uint8_t *)w.dtail;
+        a.s[i].out = w.dout;
+        a.s[i].vram = w.vram ? 1u : 0u;
+    }
     _mm_sfence();
-    __atomic_store_n(&w.ctx_n, 0u, __ATOMIC_RELEASE); /* a fresh worker caches nothing */
-    hipLaunchKernelGGL(aead_worker, dim3(1), dim3(256), 0, w.stream, w.dslot, w.dreq, (const uint4 *)w.din,
-                       w.vram ? 1u : 0u, (const uint8_t *)w.dtail, w.dout, w.seq, idle_ticks(), LIFETIME_TICKS);
+    a.group = g.dwords;
+    a.gen = __atomic_load_n(&g.gen, __ATOMIC_RELAXED) + 1u; /* never 0: the words start zeroed */
+    a.nslots = (uint32_t)g.nslots;
+    a.idle = idle_ticks();
+    a.lifetime = LIFETIME_TICKS;
+    hipLaunchKernelGGL(aead_worker, dim3(g.nslots), dim3(256), 0, g.stream, a);
     if (hipGetLastError() != hipSuccess) {
-        if (++w.launch_fails >= 3) w.state = -1;
+        if (++g.launch_fails >= 3) g.state = -1;
         return NOISE_ERROR_NOT_APPLICABLE;
     }
-    w.launch_fails = 0;
-    __atomic_add_fetch(&w.launches, 1u, __ATOMIC_RELAXED);
-    __atomic_store_n(&w.launched, true, __ATOMIC_RELEASE);
+    g.launch_fails = 0;
+    __atomic_add_fetch(&g.launches, 1u, __ATOMIC_RELAXED);
+    __atomic_store_n(&g.launched, true, __ATOMIC_RELEASE);
+    __atomic_add_fetch(&g.gen, 1u, __ATOMIC_RELEASE);
     return NOISE_ERROR_NONE;
 }
 
-/* A usable worker of device dev, locked: this thread's own if free, else
-   the first free one, else wait for this thread's own.  nullptr: none usable
+/* (by the caller of slot w, holding w.mu) make sure w's group runs: gen0 is
+   the group generation read BEFORE the caller saw it gone or leaving; if a
+   relaunch happened since, there is nothing to do. */
+std::atomic<uint32_t> g_dbg_ensure[4]; /* debug: group_ensure calls by cause (0 not launched, 1 exiting at the
+                                          call, 2 exiting while waiting), 3 of them launched nothing */
+
+int group_ensure(Worker &w, uint32_t gen0, int cause)
+{
+    WorkerGroup &g = *w.g;
+    std::lock_guard<std::mutex> gl(g.mu);
+    g_dbg_ensure[cause].fetch_add(1, std::memory_order_relaxed);
+    if (g.state != 1) return NOISE_ERROR_NOT_APPLICABLE;
+    if (__atomic_load_n(&g.gen, __ATOMIC_ACQUIRE) != gen0 && __atomic_load_n(&g.launched, __ATOMIC_ACQUIRE)) {
+        g_dbg_ensure[3].fetch_add(1, std::memory_order_relaxed);
+        return NOISE_ERROR_NONE;
+    }
+    return group_launch(g, w);
+}
+
+/* (holding w.mu) is w's group usable: recovered if drained, set up once */
+bool group_usable(Worker &w, WorkerGroup &g, int dev)
+{
+    std::lock_guard<std::mutex> gl(g.mu);
+    worker_recover(g);
+    (void)w;
+    return group_setup(g, dev) == 1;
+}
+
+/* slot n of the device's flattened order: spread over the groups first */
+Worker &slot_n(int dev, int n)
+{
+    const int ng = groups_per_dev(), ns = slots_per_group();
+    n %= ng * ns;
+    WorkerGroup &g = g_group[dev][n % ng];
+    return g.slot[(n / ng) % ns];
+}
+
+/* A usable slot of device dev, locked: this thread's own if free, else the
+   first free one, else wait for this thread's own.  nullptr: none usable
    (set up failed on all of them). */
 Worker *claim_worker(int dev, std::unique_lock<std::mutex> &lk)
 {
-    const int nw = workers_per_dev();
+    const int ng = groups_per_dev(), nw = ng * slots_per_group();
     if (t_pref < 0) t_pref = (int)(g_next_pref.fetch_add(1, std::memory_order_relaxed) % (uint32_t)nw);
-    for (int i = 0; i < nw; ++i) {
-        Worker &w = g_worker[dev][(t_pref + i) % nw];
-        std::unique_lock<std::mutex> l(w.mu, std::try_to_lock);
-        if (!l.owns_lock()) continue;
-        worker_recover(w);
-        if (worker_setup(w, dev) != 1) continue;
-        lk = std::move(l);
-        return &w;
-    }
-    for (int i = 0; i < nw; ++i) {
-        Worker &w = g_worker[dev][(t_pref + i) % nw];
-        std::unique_lock<std::mutex> l(w.mu);
-        worker_recover(w);
-        if (worker_setup(w, dev) != 1) continue;
-        lk = std::move(l);
-        return &w;
-    }
+    for (int pass = 0; pass < 2; ++pass)
+        for (int i = 0; i < nw; ++i) {
+            const int n = (t_pref + i) % nw;
+            WorkerGroup &g = g_group[dev][n % ng];
+            Worker &w = slot_n(dev, n);
+            std::unique_lock<std::mutex> l(w.mu, std::defer_lock);
+            if (pass == 0) {
+                if (!l.try_lock()) continue;
+            } else {
+                l.lock();
+            }
+            if (!group_usable(w, g, dev)) continue;
+            lk = std::move(l);
+            return &w;
+        }
     return nullptr;
 }
 
@@ -1081,9 +1286,13 @@ NA_HIDDEN void worker_park_for_batch(uint32_t workgroups)
 extern "C" NA_HIDDEN void na_worker_forget_ctx(const void *h_ctx)
 {
     for (int d = 0; d < kMaxDev; ++d)
-        for (int i = 0; i < kWorkersPerDev; ++i) {
-            Worker &w = g_worker[d][i];
-            if (worker_saw_ctx(w, h_ctx)) park_worker(w);
+        for (int i = 0; i < kMaxGroups; ++i) {
+            WorkerGroup &g = g_group[d][i];
+            for (int k = 0; k < WORKER_MAX_SLOTS; ++k)
+                if (worker_saw_ctx(g.slot[k], h_ctx)) {
+                    park_group(g);
+                    break;
+                }
         }
 }
 
@@ -1142,13 +1351,20 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     void *d_hctx = nullptr;
     if (h_ctx && hipHostGetDevicePointer(&d_hctx, (void *)h_ctx, 0) != hipSuccess)
         return NOISE_ERROR_NOT_APPLICABLE;
-    if (h_ctx) worker_note_ctx(w, h_ctx);
     const size_t ad_pad = (ad_len + 15) & ~(size_t)15;
     WorkerSlot *s = w.slot;
-    if (!w.launched || __atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE)) {
-        const int rc = worker_launch(w);
-        if (rc) return rc; /* nothing posted yet */
+    WorkerGroup &g = *w.g;
+    {   /* the generation first, then launched / exiting (group_ensure) */
+        const uint32_t gen0 = __atomic_load_n(&g.gen, __ATOMIC_ACQUIRE);
+        const bool up = __atomic_load_n(&g.launched, __ATOMIC_ACQUIRE);
+        if (!up || __atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE)) {
+            const int rc = group_ensure(w, gen0, up ? 1 : 0);
+            if (rc) return rc; /* nothing posted yet */
+        }
     }
+    /* after the launch (which starts the history afresh): this context may
+       now sit in the workgroup's LDS cache */
+    if (h_ctx) worker_note_ctx(w, h_ctx);
     const uint32_t k = ++w.seq;
     /* the input stream key || AD || pad || record (|| tag): its first head
        bytes as stamped chunks, the rest raw.  Host memory: 12 stream bytes +
@@ -1210,17 +1426,11 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     while (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
         __builtin_ia32_pause();
         if ((++spins & 1023) != 0) continue;
+        const uint32_t gen0 = __atomic_load_n(&g.gen, __ATOMIC_ACQUIRE);
         if (__atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE) && __atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != k) {
-            /* the worker left before it took k: start one at k - 1 */
-            if (hipStreamSynchronize(w.stream) != hipSuccess) {
-                w.state = -1;
-                st = NOISE_ERROR_NOT_APPLICABLE;
-                break;
-            }
-            if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == k) break;
-            w.seq = k - 1;
-            const int rc = worker_launch(w);
-            w.seq = k;
+            /* the group left before this slot took k: start it again (its
+               workgroup starts at done = k - 1 and serves k) */
+            const int rc = group_ensure(w, gen0, 2);
             if (rc) {
                 st = rc;
                 break;
@@ -1280,19 +1490,19 @@ extern "C" void noise_aead_debug_worker_fast_stamps(uint32_t *out, int n)
 extern "C" int noise_aead_debug_worker_placement(void)
 {
     const Worker *w = t_last;
-    return !w || w->state != 1 ? 0 : (w->vram ? 2 : 1);
+    return !w || w->state != 1 || !w->g || w->g->state != 1 ? 0 : (w->vram ? 2 : 1);
 }
 
-/* Test hook: the shader clock (MHz) of the last worker request's compute
-   phase (s_memtime cycles over s_memrealtime time). */
+/* Test hook: request slots of the current device whose group is resident
+   (each slot is one workgroup of its group's kernel). */
 extern "C" int noise_aead_debug_workers_resident(void)
 {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return -1;
-    for (int i = 0; i < kWorkersPerDev; ++i) {
-        Worker &w = g_worker[dev][i];
-        std::lock_guard<std::mutex> lk(w.mu);
-        if (w.state == 1 && w.launched && hipStreamQuery(w.stream) == hipErrorNotReady) ++n;
+    for (int i = 0; i < kMaxGroups; ++i) {
+        WorkerGroup &g = g_group[dev][i];
+        std::lock_guard<std::mutex> lk(g.mu);
+        if (g.state == 1 && g.launched && hipStreamQuery(g.stream) == hipErrorNotReady) n += g.nslots;
     }
     return n;
 }
@@ -1304,10 +1514,41 @@ extern "C" unsigned noise_aead_debug_worker_launches(void)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 0;
     unsigned n = 0;
-    for (int i = 0; i < kWorkersPerDev; ++i) n += __atomic_load_n(&g_worker[dev][i].launches, __ATOMIC_RELAXED);
+    for (int i = 0; i < kMaxGroups; ++i) n += __atomic_load_n(&g_group[dev][i].launches, __ATOMIC_RELAXED);
     return n;
 }
 
+/* Test hook: per group of the current device, kernels launched (out[0..n)
+   for groups 0..n-1), then the group_ensure counts by cause (debug). */
+extern "C" unsigned noise_aead_debug_worker_leave_reason(int group, int slot)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev || group < 0 || group >= kMaxGroups ||
+        slot < 0 || slot >= WORKER_MAX_SLOTS || !g_group[dev][group].slot[slot].slot)
+        return 0;
+    return g_group[dev][group].slot[slot].slot->stamps[7];
+}
+
+extern "C" void noise_aead_debug_worker_leave_info(int group, int slot, unsigned *out)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev || group < 0 || group >= kMaxGroups ||
+        slot < 0 || slot >= WORKER_MAX_SLOTS || !g_group[dev][group].slot[slot].slot)
+        return;
+    for (int i = 0; i < 4; ++i) out[i] = g_group[dev][group].slot[slot].slot->leave[i];
+}
+
+extern "C" void noise_aead_debug_worker_group_launches(unsigned *out, int n)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return;
+    for (int i = 0; i < n; ++i)
+        out[i] = i < kMaxGroups ? __atomic_load_n(&g_group[dev][i].launches, __ATOMIC_RELAXED)
+                                : (i - kMaxGroups < 4 ? g_dbg_ensure[i - kMaxGroups].load() : 0u);
+}
+
+/* Test hook: the shader clock (MHz) of the last worker request's compute
+   phase (s_memtime cycles over s_memrealtime time). */
 extern "C" double noise_aead_debug_worker_clock_mhz(void)
 {
     const WorkerSlot *s = t_last ? t_last->slot : nullptr;

@@ -142,16 +142,18 @@ def _tool(name):
 
 def test_single_calls_scale_over_threads(gpu):
     """T threads on T CipherStates make T single calls at once (each thread
-    takes a resident worker of its own, as T CPU threads would each run the
-    reference's cipherstate.c:293-410 without a lock): 8 threads reach at
-    least 4x the call rate of one (tools/mt_calls: 1400-B encrypt + decrypt
-    per iteration, every record checked).  One worker per high-priority
-    hardware queue: GPU_MAX_HW_QUEUES=8 gives the 8 threads 8 workers (the
-    HIP default of 4 caps the device at 4)."""
+    takes a request slot of its own, as T CPU threads would each run the
+    reference's cipherstate.c:293-410 without a lock): under the box's
+    default environment (4 high-priority hardware queues) 8 threads reach at
+    least 6x the call rate of one (tools/mt_calls: 1400-B encrypt + decrypt
+    per iteration, every record checked).  The worker groups take 3 of the
+    4 queues with 3 slots each (one worker per queue capped the
+    device at 4 threads)."""
     import json
     tool = _tool("mt_calls")
     rates = {}
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
+    env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "NOISE_AEAD_WORKER_QUEUES",
+                                                           "NOISE_AEAD_WORKER_SLOTS")}
     for t in (1, 8):
         r = subprocess.run([tool, "chachapoly", str(t), "1400", "1.0"], timeout=60,
                            capture_output=True, text=True, env=env)
@@ -160,7 +162,7 @@ def test_single_calls_scale_over_threads(gpu):
         assert d["ok"]
         rates[t] = d["calls_per_s"]
     print("calls/s", rates)
-    assert rates[8] >= 4 * rates[1], rates
+    assert rates[8] >= 6 * rates[1], rates
 
 
 def test_other_streams_beside_resident_workers(gpu):
@@ -169,11 +171,16 @@ def test_other_streams_beside_resident_workers(gpu):
     a memset on each of 8 newly created streams completes in well under a
     millisecond (tools/queue_probe).  A worker on a normal-priority stream
     shares a hardware queue with such streams and held them for its whole
-    5 s lifetime; the workers' high-priority streams keep them apart."""
+    5 s lifetime; the workers' high-priority streams keep them apart, and of
+    the high-priority queues the workers leave one to the application."""
     import json
     tool = _tool("queue_probe")
-    for workers in (1, 4):
-        r = subprocess.run([tool, "8", str(workers)], timeout=60, capture_output=True, text=True)
+    # normal-priority application streams (8 of them), and one high-priority
+    # stream of the application's own: the worker groups leave it the last
+    # high-priority queue (ADVICE r4)
+    for workers, streams, prio in ((1, 8, "normal"), (4, 8, "normal"), (8, 8, "normal"), (4, 1, "high"),
+                                   (8, 1, "high")):
+        r = subprocess.run([tool, str(streams), str(workers), prio], timeout=60, capture_output=True, text=True)
         assert r.returncode == 0, r.stdout + r.stderr
         d = json.loads(r.stdout.strip().splitlines()[-1])
         print(d)
@@ -206,8 +213,10 @@ def test_free_beside_concurrent_caller_parks_only_that_worker(gpu):
     """freeing an AES-GCM state parks the worker that was sent its
     context even while another thread keeps writing request headers (the
     stop word has a chunk of its own), and only that worker — the other
-    thread's worker, which never saw the context, is not relaunched."""
-    env = {"NOISE_AEAD_DEBUG_WORKER_IDLE_MS": "10000", "GPU_MAX_HW_QUEUES": "2"}
+    thread's worker, which never saw the context, is not relaunched (two
+    groups of one slot: the two threads' slots are in different groups)."""
+    env = {"NOISE_AEAD_DEBUG_WORKER_IDLE_MS": "10000", "NOISE_AEAD_WORKER_QUEUES": "2",
+           "NOISE_AEAD_WORKER_SLOTS": "1"}
     r = subprocess.run([sys.executable, "-u", os.path.join(os.path.dirname(__file__), "worker_mode_check.py"),
                         "--free-concurrent"], env=dict(os.environ, **env), timeout=110, capture_output=True,
                        text=True)

@@ -81,8 +81,9 @@ def free_check():
 
 
 def free_concurrent():
-    """--free-concurrent (run with GPU_MAX_HW_QUEUES=2 and
-    NOISE_AEAD_DEBUG_WORKER_IDLE_MS=10000): thread A keeps making ChaChaPoly
+    """--free-concurrent (run with NOISE_AEAD_WORKER_QUEUES=2,
+    NOISE_AEAD_WORKER_SLOTS=1 and NOISE_AEAD_DEBUG_WORKER_IDLE_MS=10000:
+    two groups of one slot each): thread A keeps making ChaChaPoly
     single calls (its worker stays resident, its request headers keep being
     written); the main thread's AES-GCM state S, used once from the main
     thread (the other worker caches its context), is freed.  The worker that
@@ -110,25 +111,46 @@ def free_concurrent():
                 started.set()
         cs.free()
 
+    T0 = time.time()
+    marks = []
     th = threading.Thread(target=caller)
     th.start()
     started.wait(30)
+    marks.append(time.time())
     _, st = aead.CipherState.new_by_id(0x4302)
     assert st.init_key(bytes(range(1, 33))) == 0
     st.seal(bytes(100))
+    marks.append(time.time())
     time.sleep(0.05)
+    import ctypes as C
+
+    def per_group():
+        a = (C.c_uint * 12)()
+        lib.noise_aead_debug_worker_group_launches(a, 12)
+        return list(a)
+    g0 = per_group()
     res0, l0 = lib.noise_aead_debug_workers_resident(), lib.noise_aead_debug_worker_launches()
     st.free()
     t0 = time.time()
     while lib.noise_aead_debug_workers_resident() >= res0 and time.time() - t0 < 0.5:
         time.sleep(0.001)
     res1 = lib.noise_aead_debug_workers_resident()
+    marks.append(time.time())
     time.sleep(0.1)
     l1 = lib.noise_aead_debug_worker_launches()
     stop[0] = True
     th.join()
     ok = res0 == 2 and res1 == 1 and l1 == l0 and not errs
     print("resident", res0, res1, "launches", l0, l1, "errs", errs[:3])
+    print("per group + ensure causes", g0, per_group())
+    lib.noise_aead_debug_worker_leave_reason.restype = C.c_uint
+    print("leave reasons g0 g1", lib.noise_aead_debug_worker_leave_reason(0, 0),
+          lib.noise_aead_debug_worker_leave_reason(1, 0))
+    for gi in (0, 1):
+        a = (C.c_uint * 4)()
+        lib.noise_aead_debug_worker_leave_info(gi, 0, a)
+        print("leave info", gi, list(a), "age_s", ((a[1] - a[0]) & 0xffffffff) / 1e8)
+    print("timeline", [round(x - T0, 3) for x in marks])
     print("parked_ok", 1 if ok else 0)
     return 0 if ok else 1
 

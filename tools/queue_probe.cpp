@@ -3,11 +3,17 @@
 // worker stays resident); meanwhile the main thread creates streams one by
 // one and times a small hipMemsetAsync on each (enqueue -> complete).  A
 // stream that shares a hardware queue with the resident worker waits for the
-// worker to leave.  Prints one JSON line.  Build: tools/build_latency.sh.
+// worker to leave.  prio "high": the application's streams are
+// high-priority ones, the pool the workers' streams come from:
+// the library leaves one queue of that pool to the application.  Prints one
+// JSON line.  Build: tools/build_latency.sh.
+//
+//   queue_probe [streams] [worker threads] [normal|high]
 #include <hip/hip_runtime.h>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <thread>
 #include <vector>
 #include "noise_aead_hip.h"
@@ -21,6 +27,7 @@ int main(int argc, char **argv)
 {
     const int nstreams = argc > 1 ? atoi(argv[1]) : 8;
     const int workers = argc > 2 ? atoi(argv[2]) : 1;
+    const bool high = argc > 3 && !strcmp(argv[3], "high");
     std::atomic<bool> stop{false};
     std::atomic<long> calls{0};
     std::vector<std::thread> th;
@@ -47,7 +54,13 @@ int main(int argc, char **argv)
     std::vector<hipStream_t> ss;
     for (int i = 0; i < nstreams; ++i) {
         hipStream_t s;
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 1;
+        if (high) {
+            int least = 0, greatest = 0;
+            if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return 1;
+            if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) != hipSuccess) return 1;
+        } else if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+            return 1;
+        }
         ss.push_back(s);
         const double t0 = now_us();
         if (hipMemsetAsync(d, i, 1 << 20, s) != hipSuccess) return 1;
@@ -56,7 +69,8 @@ int main(int argc, char **argv)
     }
     stop.store(true);
     for (auto &t : th) t.join();
-    printf("{\"streams\": %d, \"worker_threads\": %d, \"calls\": %ld, \"memset_us\": [", nstreams, workers, calls.load());
+    printf("{\"streams\": %d, \"priority\": \"%s\", \"worker_threads\": %d, \"calls\": %ld, \"memset_us\": [",
+           nstreams, high ? "high" : "normal", workers, calls.load());
     for (size_t i = 0; i < us.size(); ++i) printf("%s%.1f", i ? ", " : "", us[i]);
     printf("]}\n");
     for (auto s : ss) (void)hipStreamDestroy(s);
