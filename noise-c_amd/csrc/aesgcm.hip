@@ -600,7 +600,8 @@ NA_DEV uint32_t te_lookup(const uint8_t *te, uint32_t s, uint32_t lane_tpl)
     return *(const uint32_t *)(te + addr);
 }
 
-NA_DEV void aes256_lds(const uint8_t *L, const uint32_t *rk, uint32_t tpl, uint32_t &s0,
+template <typename RK>
+NA_DEV void aes256_lds(const uint8_t *L, RK rk, uint32_t tpl, uint32_t &s0,
                        uint32_t &s1, uint32_t &s2, uint32_t &s3)
 {
     s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
@@ -629,7 +630,8 @@ NA_DEV void aes256_lds(const uint8_t *L, const uint32_t *rk, uint32_t tpl, uint3
     s0 = o0 ^ rk[56]; s1 = o1 ^ rk[57]; s2 = o2 ^ rk[58]; s3 = o3 ^ rk[59];
 }
 
-NA_DEV void aes_ctr_lds(const uint8_t *te, const uint32_t *rk, uint32_t tpl, uint32_t n_hi,
+template <typename RK>
+NA_DEV void aes_ctr_lds(const uint8_t *te, RK rk, uint32_t tpl, uint32_t n_hi,
                         uint32_t n_lo, uint32_t ctr, uint32_t ks[4])
 {
     uint32_t s0 = 0, s1 = n_hi, s2 = n_lo, s3 = ctr;
@@ -652,7 +654,8 @@ struct AesPre {
     uint32_t d0, d1, d2, d3; /* round 2, each column's two constant lookups + key */
 };
 
-NA_DEV AesPre aes_pre_lds(const uint8_t *L, const uint32_t *rk, uint32_t tpl, uint32_t n_hi,
+template <typename RK>
+NA_DEV AesPre aes_pre_lds(const uint8_t *L, RK rk, uint32_t tpl, uint32_t n_hi,
                           uint32_t n_lo)
 {
     const uint32_t s0 = rk[0], s1 = n_hi ^ rk[1], s2 = n_lo ^ rk[2], s3 = rk[3];
@@ -675,7 +678,8 @@ NA_DEV AesPre aes_pre_lds(const uint8_t *L, const uint32_t *rk, uint32_t tpl, ui
 
 /* E_K(0^32 || BE64(n) || BE32(ctr)) from the record's AesPre (ctr < 2^16),
    as little-endian memory words; equals aes_ctr_lds. */
-NA_DEV void aes_ctr_pre(const uint8_t *L, const uint32_t *rk, uint32_t tpl, const AesPre &p,
+template <typename RK>
+NA_DEV void aes_ctr_pre(const uint8_t *L, RK rk, uint32_t tpl, const AesPre &p,
                         uint32_t ctr, uint32_t ks[4])
 {
     const uint32_t s3 = ctr ^ rk[3];
@@ -717,8 +721,8 @@ NA_DEV uint32_t blk_mask(uint32_t nb, int w)
 
 /* CTR over one lane's data blocks d = d0, d0 + K, ... < M of a record, src to
    dst: the decrypt pass of a VERIFY_FIRST open, after the tag verified. */
-template <bool FAST = true>
-NA_DEV void gcm_ctr_lane(const uint8_t *TE, const uint32_t *rk, uint32_t tpl, const AesPre &pre,
+template <bool FAST = true, typename RK = const uint32_t *>
+NA_DEV void gcm_ctr_lane(const uint8_t *TE, RK rk, uint32_t tpl, const AesPre &pre,
                          const uint8_t *src, uint8_t *dst, uint32_t len, uint32_t d0, uint32_t M,
                          uint32_t K)
 {
@@ -743,9 +747,9 @@ NA_DEV void gcm_ctr_lane(const uint8_t *TE, const uint32_t *rk, uint32_t tpl, co
 /* This thread's record of block blk (records [blk * 256, blk * 256 + 256))
    of a uniform staged job, with the T-tables at TE and the state's
    multiply-by-H^4 table and round keys (h4_lds, rk) in LDS. */
-template <bool OPEN, bool CT>
+template <bool OPEN, bool CT, typename RK>
 NA_DEV void gcm_staged_rec(const UniformArgs &a, const uint8_t *TE, const uint4 *h4_lds,
-                           const uint32_t *rk, uint32_t blk)
+                           RK rk, uint32_t blk)
 {
     constexpr int K = GCM_LANES;
     const uint32_t rec0 = blk * (uint32_t)GCM_WG_RECS;
@@ -909,6 +913,30 @@ __global__ __launch_bounds__(GCM_WG) void gcm_duplex_staged(UniformArgs s, Unifo
    record as soon as its seal record is done, so a CU's SIMDs stay busy
    through the first half's uneven finish and the workgroup drains once, not
    twice.  Results are those of the separate kernels (same per-record code). */
+/* Round keys through the scalar cache.  Where a wave's records share one
+   state its 60 round-key words are wave-uniform: read with s_load from the
+   context in global memory they cost no LDS cycle, where the LDS copy costs
+   15 ds_read_b128 per block (≈10 % of the kernel's LDS cycles).  The
+   compiler reloads them per block (48 of 60 words: six s_load_dwordx8) and
+   a scalar load's wait is lgkmcnt(0), which also drains the LDS lookups in
+   flight: measured (profiles/r05/rk_scalar_ab.txt) the ragged seal gains
+   3.5 % (0.787 -> 0.760 ms at C5), the verify-first ragged open loses 14 %
+   and C3's fused duplex 1.5 %, so only the ragged seal takes it.
+   NA_RK_SCALAR=0: the LDS copy everywhere (A/B). */
+#ifndef NA_RK_SCALAR
+#define NA_RK_SCALAR 1
+#endif
+typedef const __attribute__((address_space(4))) uint32_t *RkS;
+
+/* the wave-uniform address p as a constant-address-space pointer */
+NA_DEV RkS rk_scalar(const uint32_t *p)
+{
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return (RkS)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 struct GcmLds2 {
     uint32_t te[2][256][64];
     uint4 h4[2][GHASH_TAB_ENTRIES];
@@ -1254,9 +1282,9 @@ struct GcmLdsR {
 /* One record, 4 lanes (l = 0..3): gcm_staged's GHASH/CTR core with the
    record's tables passed in; FAST as in chachapoly.hip (16-B aligned record,
    input readable to roundup16). */
-template <bool OPEN, bool FAST, bool CT, int KL = GCM_LANES>
+template <bool OPEN, bool FAST, bool CT, int KL = GCM_LANES, typename RK = const uint32_t *>
 NA_DEV bool gcm_record_staged(const GcmView &rv, int l, const uint8_t *TE, uint32_t tpl,
-                              const uint32_t *rk, const uint4 *h4, bool vf)
+                              RK rk, const uint4 *h4, bool vf)
 {
     /* KL lanes per record (4, or 8 with the H^8 Horner table): the Horner
        step is H^KL, h4 its multiply table */
@@ -1441,7 +1469,19 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
         bool ok;
         const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
         const bool vf = OPEN && a.vf;
-        if (sl >= 0)
+        bool done = false;
+#if NA_RK_SCALAR
+        if constexpr (!OPEN) { /* seals only: measured slower in the opens and in C3's fused duplex */
+            const int s0 = __builtin_amdgcn_readfirstlane(sl);
+            if (s0 >= 0 && __all(sl == s0)) { /* the wave's records share an LDS slot */
+                ok = gcm_record_staged<OPEN, FAST, CT, KL>(
+                    rv, l, TE, tpl, rk_scalar(((const AesCtx *)(a.keys + slot_off[s0]))->rk), L.h4[s0], vf);
+                done = true;
+            }
+        }
+#endif
+        if (done) {
+        } else if (sl >= 0)
             ok = gcm_record_staged<OPEN, FAST, CT, KL>(rv, l, TE, tpl, L.rk[sl], L.h4[sl], vf);
         else /* a third state in the window: its own context, from global memory */
             ok = gcm_record_global<OPEN, FAST, CT, KL>(rv, l, TE, tpl, vf);
