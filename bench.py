@@ -438,6 +438,11 @@ def parse_args():
                     help="opens with NOISE_AEAD_FLAG_VERIFY_FIRST (authenticate, then decrypt)")
     ap.add_argument("--c5-streams", type=int, default=2, choices=(1, 2),
                     help="C5: 2 = the AES-GCM and ChaChaPoly halves on two streams, concurrently")
+    ap.add_argument("--c5-prio", default="none", choices=("none", "aes", "chacha"),
+                    help="C5 with two streams: the half whose stream is high-priority")
+    ap.add_argument("--c5-join", default="step", choices=("step", "phase"),
+                    help="C5 with two streams: each cipher's open follows its own seal and the halves "
+                         "join once per step (step), or both seals finish before either open (phase)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group plumbing only, no GPU work (CPU tests)")
     return ap.parse_args()
@@ -1002,14 +1007,37 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                             flags=A.FLAG_FAST | (oflags if open_ else 0), stream=stream)
 
     # Two streams: the LDS-bound AES-GCM kernel and the VALU-bound ChaChaPoly
-    # kernel share the CUs instead of running back to back; the open phase
-    # waits for both seals (fork/join by events, no host sync).
+    # kernel share the CUs instead of running back to back (fork/join by
+    # events, no host sync).  --c5-join step (default): each cipher's open
+    # depends only on its own seal, as the records do, so one half's open
+    # fills the CUs the other half's seal leaves in its tail; the halves
+    # join at the end of the step.  phase: both seals finish before either
+    # open (round 4's shape).
     main_s = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(dev) if args.c5_streams == 2 and len(groups) == 2 else None
+    side = torch.cuda.Stream(dev, priority=-1 if args.c5_prio == "aes" else 0) \
+        if args.c5_streams == 2 and len(groups) == 2 else None  # the AES-GCM half
+    cha_s = torch.cuda.Stream(dev, priority=-1) if side is not None and args.c5_prio == "chacha" else None
     fork = [torch.cuda.Event() for _ in range(2)]
     join = [torch.cuda.Event() for _ in range(2)]
 
     def step():
+        if side is not None and args.c5_join == "step":
+            fork[0].record(main_s)
+            side.wait_event(fork[0])
+            cs = main_s
+            if cha_s is not None:
+                cha_s.wait_event(fork[0])
+                cs = cha_s
+            rc = launch(groups[1], False, side.cuda_stream) or launch(groups[0], False, cs.cuda_stream) \
+                or launch(groups[1], True, side.cuda_stream) or launch(groups[0], True, cs.cuda_stream)
+            if rc:
+                raise RuntimeError(f"launch failed {rc:#x}")
+            join[0].record(side)
+            main_s.wait_event(join[0])
+            if cha_s is not None:
+                join[1].record(cha_s)
+                main_s.wait_event(join[1])
+            return
         for open_ in (False, True):
             if side is None:
                 for g in groups:
@@ -1110,6 +1138,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
         "config": {"workload": cfg["workload"], "config": "c5", "records_per_gpu": R,
                    "states_per_gpu": S, "payload_bytes_per_step": int(2 * payload * world),
                    "streams": 2 if side is not None else 1,
+                   "join": args.c5_join if side is not None else None,
                    "parallelism": f"states x{world}",
                    "settle": {"ms": args.settle_ms, "steps": settled[0], "s": round(settled[1], 3)}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
