@@ -69,7 +69,10 @@ NA_DEV bool seg_ok(const void *p, uint32_t n, uint32_t kind, uint32_t info)
 
 /* Blocks per lane a ragged record aims at (K = the smallest power of two with
    ceil(B/K) <= SEG_TARGET, at most SEG_KMAX) */
-constexpr uint32_t SEG_TARGET = 32;
+#ifndef NA_SEG_TARGET
+#define NA_SEG_TARGET 32
+#endif
+constexpr uint32_t SEG_TARGET = NA_SEG_TARGET;
 constexpr uint32_t SEG_KMAX = 16;
 constexpr uint32_t SEG_BUCKETS = 1025; /* J = 0 .. 1024 (65519-byte records) */
 

@@ -20,3 +20,5 @@ case "$G" in *" write "*) run write WRITE_SIZE || exit 1;; esac
 case "$G" in *" sq "*) run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS GRBM_GUI_ACTIVE || exit 1;; esac
 case "$G" in *" busy "*) run busy SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY || exit 1;; esac
 case "$G" in *" tcc "*) run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum || exit 1;; esac
+# LDS: array cycles, bank-conflict cycles, issue stalls (opt-in: PMC_GROUPS="lds")
+case "$G" in *" lds "*) run lds SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE || exit 1;; esac
