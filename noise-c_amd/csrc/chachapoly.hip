@@ -1408,6 +1408,70 @@ NA_DEV void solo_auth(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
     }
 }
 
+/* The AUTH pass with the ciphertext loaded straight into registers instead
+   of through the LDS tiles: each lane reads its own record's 128-B step with
+   eight 16-B loads (whole 128-B lines), D steps in flight (D x 32 VGPRs,
+   free during this pass: the kernel's allocation is set by the ChaCha
+   passes).  The tiles' two steps in flight left the pass latency-bound —
+   ~50 us of a ~120 us C2 verify-first duplex launch
+   (profiles/r04/timeline/timeline_solo.txt) during which the SIMD's other
+   wave issued alone.  Measured slower (profiles/r05/auth_reg_ab.txt: C2
+   verify-first 1412-1428 GiB/s at D = 2, 3, 4, 6 against 1462-1464 through
+   the tiles; one pass 1626-1629): the per-lane loads touch 64 lines per
+   instruction where the tile DMA moves 8 whole 128-B runs.  Kept as the
+   A/B (NA_AUTH_REG=D); the default is the tile pass (0). */
+#ifndef NA_AUTH_REG
+#define NA_AUTH_REG 0
+#endif
+#if NA_AUTH_REG
+template <int D>
+NA_DEV void solo_auth_reg(const UniformArgs &a, const SoloRec &q, const R32 &r, P32 &h)
+{
+    const uint8_t *src = u_src(a, q.rc);
+    uint4 buf[D][8];
+    /* step m's 8 chunks; chunks at or past lim (64 J: readable in a FAST
+       slot) re-read the record's first chunk and are never used */
+    auto load = [&](uint4 *b, uint32_t m) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t off = 128u * m + 16u * (uint32_t)i;
+            if (off >= q.lim) off = 0;
+            b[i] = *(const uint4 *)(src + off);
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(buf[d], (uint32_t)d);
+    for (uint32_t m0 = 0; m0 < q.S; m0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const uint32_t m = m0 + (uint32_t)d;
+            if (m < q.S) {
+                __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+                for (uint32_t u = 0; u < 2; ++u) {
+                    const uint32_t j = 2 * m + u;
+                    if (j < q.J) {
+                        uint32_t w[16];
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const uint4 v = buf[d][4 * u + c];
+                            w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+                        }
+                        uint32_t nb = 4;
+                        if (j == q.J - 1) {
+                            mask_unit(w, q.tail);
+                            nb = (q.tail + 15) / 16;
+                        }
+                        p32_unit(h, r, w, nb);
+                    }
+                }
+                if (m + D < q.S) load(buf[d], m + D);
+            }
+        }
+    }
+}
+#endif
+
 /* Open, one pass: Poly1305 over each ciphertext unit as it arrives, then
    the plaintext out; a wave holding a rejected record repairs it after the
    verdict exactly as open_il_staged does (in place: XOR with the key stream
@@ -1427,12 +1491,20 @@ NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
     u_key_nonce<UKEY>(a, rec0, rc, key, n_lo, n_hi);
     ChaPre pre;
     chacha_pre(key, n_lo, n_hi, pre);
+#if NA_AUTH_REG
+    if (S && !a.vf) solo_dma(a, rec0, lane, 0, lim, tiles);
+#else
     if (S) solo_dma(a, rec0, lane, 0, lim, tiles);
+#endif
     R32 r;
     uint32_t s[4];
     P32 h;
     solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, rc) : nullptr, a.ad_len, r, s, h);
+#if NA_AUTH_REG
+    if (a.vf) solo_auth_reg<NA_AUTH_REG>(a, q, r, h);
+#else
     if (a.vf) solo_auth(a, q, tiles, r, h);
+#endif
     else solo_pass<SOLO_OPEN1>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
     uint32_t tag[4], got[4];
     solo_tag(h, r, a.ad_len, len, s, tag);
