@@ -440,6 +440,8 @@ def parse_args():
                     help="C5: 2 = the AES-GCM and ChaChaPoly halves on two streams, concurrently")
     ap.add_argument("--c5-prio", default="none", choices=("none", "aes", "chacha"),
                     help="C5 with two streams: the half whose stream is high-priority")
+    ap.add_argument("--c5-first", default="aes", choices=("aes", "chacha"),
+                    help="C5 with two streams and --c5-join step: the half launched first")
     ap.add_argument("--c5-join", default="step", choices=("step", "phase"),
                     help="C5 with two streams: each cipher's open follows its own seal and the halves "
                          "join once per step (step), or both seals finish before either open (phase)")
@@ -1028,8 +1030,12 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
             if cha_s is not None:
                 cha_s.wait_event(fork[0])
                 cs = cha_s
-            rc = launch(groups[1], False, side.cuda_stream) or launch(groups[0], False, cs.cuda_stream) \
-                or launch(groups[1], True, side.cuda_stream) or launch(groups[0], True, cs.cuda_stream)
+            if args.c5_first == "chacha":
+                rc = launch(groups[0], False, cs.cuda_stream) or launch(groups[0], True, cs.cuda_stream) \
+                    or launch(groups[1], False, side.cuda_stream) or launch(groups[1], True, side.cuda_stream)
+            else:
+                rc = launch(groups[1], False, side.cuda_stream) or launch(groups[0], False, cs.cuda_stream) \
+                    or launch(groups[1], True, side.cuda_stream) or launch(groups[0], True, cs.cuda_stream)
             if rc:
                 raise RuntimeError(f"launch failed {rc:#x}")
             join[0].record(side)

@@ -67,6 +67,33 @@ NA_DEV bool seg_ok(const void *p, uint32_t n, uint32_t kind, uint32_t info)
 #define SEG_OK(p, n, kind, info) true
 #endif
 
+/* NA_SEG_TL (A/B variant builds only): per-wave cycle accounting of the
+   persistent ragged kernel (s_memtime, wave-uniform): [0] the wave's life,
+   [1] job set-up (ticket, plan entry, descriptor, key, owner table), [2]
+   the first step's wait for its DMA, [3] the other steps' waits, [4] the
+   passes, [5] combine + tag, [6] the end-of-job store drain, [7] jobs.  Each
+   wave writes its row of g_seg_tlw at exit (last launch wins);
+   noise_aead_debug_seg_tl sums them. */
+#ifdef NA_SEG_TL
+__device__ unsigned long long g_seg_tlw[4096][8];
+struct SegTL {
+    uint64_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    NA_DEV static uint64_t now() { return __builtin_amdgcn_s_memtime(); }
+    NA_DEV void add(int k, uint64_t v) { c[k] += v; }
+    NA_DEV void flush()
+    {
+        if ((threadIdx.x & 63) == 0)
+            for (int k = 0; k < 8; ++k) g_seg_tlw[blockIdx.x * 4 + (threadIdx.x >> 6)][k] = c[k];
+    }
+};
+#else
+struct SegTL {
+    NA_DEV static uint64_t now() { return 0; }
+    NA_DEV void add(int, uint64_t) {}
+    NA_DEV void flush() {}
+};
+#endif
+
 /* Blocks per lane a ragged record aims at (K = the smallest power of two with
    ceil(B/K) <= SEG_TARGET, at most SEG_KMAX) */
 #ifndef NA_SEG_TARGET
@@ -373,11 +400,13 @@ NA_DEV void seg_data(const SegLane &q, uint32_t j, uint32_t w[16], const uint32_
 template <int MODE, bool PRIO, bool FIRST, class IO>
 NA_DEV void seg_step(const SegLane &q, const IO &io, uint32_t lane, uint32_t m, uint32_t S, uint4 *tiles,
                      const uint32_t key[8], const ChaPre &pre, R32 &r, uint32_t rw[4], uint32_t s[4],
-                     P32 &h, uint32_t okm, bool ok)
+                     P32 &h, uint32_t okm, bool ok, SegTL &tl)
 {
     uint4 *cur = tiles + SOLO_TILE * (m & 1), *nxt = tiles + SOLO_TILE * ((m + 1) & 1);
     uint32_t wu[2][16];
+    const uint64_t tw = SegTL::now();
     solo_wait();
+    tl.add(FIRST ? 2 : 3, SegTL::now() - tw);
     solo_get(cur, lane, 0, wu[0]);
     solo_get(cur, lane, 1, wu[1]);
     if (!FIRST && m >= 1) io.store(lane, m - 1, nxt, okm);
@@ -433,19 +462,21 @@ NA_DEV void seg_step(const SegLane &q, const IO &io, uint32_t lane, uint32_t m, 
 template <int MODE, bool PRIO, class IO>
 NA_DEV void seg_pass(const SegLane &q, const IO &io, uint32_t lane, uint32_t S, uint4 *tiles,
                      const uint32_t key[8], const ChaPre &pre, R32 &r, uint32_t rw[4], uint32_t s[4],
-                     P32 &h, uint32_t okm, bool ok)
+                     P32 &h, uint32_t okm, bool ok, SegTL &tl)
 {
+    const uint64_t t0 = SegTL::now();
     uint32_t m0 = 0;
     if (MODE != SEG_DEC && S) {
-        seg_step<MODE, PRIO, true>(q, io, lane, 0u, S, tiles, key, pre, r, rw, s, h, okm, ok);
+        seg_step<MODE, PRIO, true>(q, io, lane, 0u, S, tiles, key, pre, r, rw, s, h, okm, ok, tl);
         m0 = 1;
     }
     for (uint32_t m = m0; m < S; ++m)
-        seg_step<MODE, PRIO, false>(q, io, lane, m, S, tiles, key, pre, r, rw, s, h, okm, ok);
+        seg_step<MODE, PRIO, false>(q, io, lane, m, S, tiles, key, pre, r, rw, s, h, okm, ok, tl);
     if (S) {
         __builtin_amdgcn_wave_barrier();
         io.store(lane, S - 1, tiles + SOLO_TILE * ((S - 1) & 1), okm);
     }
+    tl.add(4, SegTL::now() - t0);
 }
 
 /* The verify-first AUTH pass: r from the leader's key block first, then
@@ -592,7 +623,7 @@ NA_DEV void seg_repair(const SegLane &q, const IO &io, uint32_t lane, uint32_t S
    open. */
 template <bool OPEN, bool PRIO, class IO>
 NA_DEV void seg_job(const SegLane &q, const uint32_t key[8], const IO &io, uint32_t lane, uint4 *tiles,
-                    uint8_t *status, bool vf, bool inplace)
+                    uint8_t *status, bool vf, bool inplace, SegTL &tl)
 {
     const uint32_t S = wave_max((q.nb + 1) / 2);
     const uint32_t kmax = wave_max(q.K);
@@ -603,7 +634,8 @@ NA_DEV void seg_job(const SegLane &q, const uint32_t key[8], const IO &io, uint3
     P32 h = p32_zero();
     if (S) io.dma(lane, 0, tiles);
     if (!OPEN) {
-        seg_pass<SEG_SEAL, PRIO>(q, io, lane, S, tiles, key, pre, r, rw, s, h, 0xffu, true);
+        seg_pass<SEG_SEAL, PRIO>(q, io, lane, S, tiles, key, pre, r, rw, s, h, 0xffu, true, tl);
+        const uint64_t tc = SegTL::now();
         const Fe acc = seg_combine(q, rw, h, kmax);
         if (q.live && q.k == 0) {
             uint32_t tag[4];
@@ -611,10 +643,11 @@ NA_DEV void seg_job(const SegLane &q, const uint32_t key[8], const IO &io, uint3
             if (SEG_OK(q.dst + q.len, 16, 5, q.rec)) tag_out(q.dst + q.len, q.len, tag);
             if (status && SEG_OK(status + q.rec, 1, 6, q.rec)) status[q.rec] = 0;
         }
+        tl.add(5, SegTL::now() - tc);
         return;
     }
     if (vf) seg_auth(q, io, lane, S, tiles, key, pre, r, rw, s, h);
-    else seg_pass<SEG_OPEN1, PRIO>(q, io, lane, S, tiles, key, pre, r, rw, s, h, 0xffu, true);
+    else seg_pass<SEG_OPEN1, PRIO>(q, io, lane, S, tiles, key, pre, r, rw, s, h, 0xffu, true, tl);
     const Fe acc = seg_combine(q, rw, h, kmax);
     bool okl = false;
     if (q.live && q.k == 0) {
@@ -631,7 +664,7 @@ NA_DEV void seg_job(const SegLane &q, const uint32_t key[8], const IO &io, uint3
         const uint32_t okm = seg_owner_mask(ok, lane);
         __builtin_amdgcn_wave_barrier(); /* the AUTH pass's tile reads are done */
         if (S) io.dma(lane, 0, tiles);
-        seg_pass<SEG_DEC, PRIO>(q, io, lane, S, tiles, key, pre, r, rw, s, h, okm, ok);
+        seg_pass<SEG_DEC, PRIO>(q, io, lane, S, tiles, key, pre, r, rw, s, h, okm, ok, tl);
         return;
     }
     const bool bad = q.live && !ok;
@@ -678,8 +711,9 @@ __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seg2_uniform(Unifo
     SegIOU io;
     io.init(a, job * 32u, q, lane);
     const bool inplace = a.in == a.out && a.in_stride == a.out_stride;
+    SegTL tl;
     seg_job<OPEN, true>(q, key, io, lane, tiles[threadIdx.x >> 6], OPEN ? a.status : nullptr, a.vf != 0,
-                        inplace);
+                        inplace, tl);
 }
 
 /* ----------------------------------------------------------------- ragged */
@@ -785,12 +819,19 @@ __global__ __launch_bounds__(1024) void seg_plan_place(const RecDesc *recs, uint
 
 /* The lane's segment of plan job `job` (SEG_IDLE lanes: live = false, a
    copy of the wave's first record for addresses) */
-NA_DEV SegLane seg_ragged_lane(const RaggedArgs &a, const uint32_t *map, uint32_t total, uint32_t job,
-                               uint32_t lane, uint32_t key[8])
+/* the plan entries of job `job` for this lane: e (SEG_IDLE past the
+   plan's lanes) and the job's first lane's, e0 (always placed); a job at
+   or past n_jobs reads nothing */
+NA_DEV void seg_map_entries(const uint32_t *map, uint32_t total, uint32_t n_jobs, uint32_t job, uint32_t lane,
+                            uint32_t &e, uint32_t &e0)
 {
     const uint32_t gl = 64u * job + lane;
-    uint32_t e = gl < total && SEG_OK(map + gl, 4, 9, gl) ? map[gl] : SEG_IDLE;
-    const uint32_t e0 = SEG_OK(map + 64u * job, 4, 9, job) ? map[64u * job] : 0u; /* the job's first lane is always placed */
+    e = job < n_jobs && gl < total && SEG_OK(map + gl, 4, 9, gl) ? map[gl] : SEG_IDLE;
+    e0 = job < n_jobs && SEG_OK(map + 64u * job, 4, 9, job) ? map[64u * job] : 0u;
+}
+
+NA_DEV SegLane seg_ragged_lane(const RaggedArgs &a, uint32_t e, uint32_t e0, uint32_t key[8])
+{
     SegLane q;
     q.live = e != SEG_IDLE;
     if (!q.live) e = e0 & ~63u;
@@ -827,22 +868,40 @@ __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seg_ragged(RaggedA
     auto &owners = sh.owners;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t n_jobs = p->n_jobs, total = p->total_lanes;
+    SegTL tl;
+    const uint64_t born = SegTL::now();
+    /* the next job's ticket and plan entries are taken while the current
+       job runs: a job's set-up was four dependent round trips (ticket, plan,
+       descriptor, key), 8-9 % of a wave's life (tools/seg_tl.py) */
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(&p->ticket, 1u);
+    uint32_t t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tk, 0, 64));
+    uint32_t e_nx, e0_nx;
+    seg_map_entries(map, total, n_jobs, t, lane, e_nx, e0_nx);
     for (;;) {
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd(&p->ticket, 1u);
-        t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)t, 0, 64));
+        const uint64_t t0 = SegTL::now();
         if (t >= n_jobs) break; /* every wave draws one ticket past the end */
+        const uint32_t e = e_nx, e0 = e0_nx;
+        if (lane == 0) tk = atomicAdd(&p->ticket, 1u);
         uint32_t key[8];
-        SegLane q = seg_ragged_lane(a, map, total, t, lane, key);
+        SegLane q = seg_ragged_lane(a, e, e0, key);
+        t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tk, 0, 64));
+        seg_map_entries(map, total, n_jobs, t, lane, e_nx, e0_nx);
         seg_blocks(q);
         SegIOL io;
         io.tab = owners[w];
         io.init(q, lane);
         const bool inplace = q.src == q.dst;
-        seg_job<OPEN, false>(q, key, io, lane, tiles[w], a.status, a.vf != 0, inplace);
+        tl.add(1, SegTL::now() - t0);
+        seg_job<OPEN, false>(q, key, io, lane, tiles[w], a.status, a.vf != 0, inplace, tl);
+        const uint64_t td = SegTL::now();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the job's stores left before the tile is reused */
         __builtin_amdgcn_wave_barrier();
+        tl.add(6, SegTL::now() - td);
+        tl.add(7, 1);
     }
+    tl.add(0, SegTL::now() - born);
+    tl.flush();
 }
 
 } // namespace na

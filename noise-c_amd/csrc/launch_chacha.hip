@@ -290,3 +290,29 @@ extern "C" int noise_aead_debug_seg_viol(uint64_t *out, int n)
     return (int)cnt;
 }
 #endif
+
+#ifdef NA_SEG_TL
+/* debug variant only: the per-wave cycle accounts of the last persistent
+   ragged launch (chachapoly_seg.hip SegTL), summed over waves into out[8];
+   reset != 0 zeroes them afterwards.  Returns the waves that ran. */
+extern "C" int noise_aead_debug_seg_tl(uint64_t *out, int reset)
+{
+    static unsigned long long h[4096][8];
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(na::g_seg_tlw), sizeof(h), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    int waves = 0;
+    for (int k = 0; k < 8; ++k) out[k] = 0;
+    for (int w = 0; w < 4096; ++w) {
+        if (!h[w][0]) continue;
+        ++waves;
+        for (int k = 0; k < 8; ++k) out[k] += h[w][k];
+    }
+    if (reset) {
+        static unsigned long long z[4096][8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(na::g_seg_tlw), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+            return -1;
+    }
+    return waves;
+}
+#endif
