@@ -69,14 +69,14 @@ def test_default_layout_and_kernel_names():
 def test_c5_profile_names():
     """C5's dominant kernels as bench.run_mixed names them (the library's
     gcm_ragged_shape policy at 64 Ki AES records per GPU: 1024 threads, two
-    records per 8-lane group) are in the committed C5 profile."""
+    records per 8-lane group; the segmented persistent ChaChaPoly kernel for
+    64 Ki ragged FAST records) are in the committed C5 profile."""
     import json
     with open(os.path.join(ROOT, "profiles", "traffic_c5.json")) as f:
         kernels = json.load(f)["kernels"]
     for open_ in ("true", "false"):
         assert f"gcm_ragged_staged<{open_}, true, 1024, false, 2, 8>" in kernels
-    assert "chachapoly_open_ragged<8, true, false>" in kernels or \
-        "chachapoly_open_ragged<8, true>" in kernels
+        assert f"chachapoly_seg_ragged<{open_}>" in kernels
 
 
 def _bench(args, env=None, timeout=240):
