@@ -574,6 +574,10 @@ def main():
                                                 wl.in_stride, wl.out_stride, wl.sh, wl.sets, wl.seal)
         except Exception as e:
             result["scatter_gather"] = {"error": repr(e)}
+        # a failed scatter/gather is stated at the top level of
+        # the line (it still never voids the GPU number)
+        sgr = result["scatter_gather"]
+        result["scatter_gather_ok"] = "error" not in sgr and bool(sgr.get("verified", sgr.get("ok", False)))
     if world > 1 and not args.no_n1 and args.n1_value is None:
         result["n1_in_run"] = n1_reference(args, cfg, A, torch, dev, rank, dist, wl, N, S, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1167,6 +1171,10 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                                                       lay, pt, groups, launch)
         except Exception as e:
             result["scatter_gather"] = {"error": repr(e)}
+        # a failed scatter/gather is stated at the top level of
+        # the line (it still never voids the GPU number)
+        sgr = result["scatter_gather"]
+        result["scatter_gather_ok"] = "error" not in sgr and bool(sgr.get("verified", sgr.get("ok", False)))
     if world > 1 and not args.no_n1 and args.n1_value is None:
         dist.barrier()  # rank 0 alone on its own shard: the in-run N = 1 value
         v = 2.0 * payload * args.steps / timed(None) / GIB if rank == 0 else 0.0
