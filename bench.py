@@ -440,6 +440,9 @@ def parse_args():
                     help="C5: 2 = the AES-GCM and ChaChaPoly halves on two streams, concurrently")
     ap.add_argument("--c5-prio", default="none", choices=("none", "aes", "chacha"),
                     help="C5 with two streams: the half whose stream is high-priority")
+    ap.add_argument("--c5-sets", type=int, default=1, choices=(1, 2),
+                    help="C5 with two streams and --c5-join step: 2 = each step seals one set and opens "
+                         "the set sealed the step before (four independent launches, as C2-C4's duplex)")
     ap.add_argument("--c5-first", default="aes", choices=("aes", "chacha"),
                     help="C5 with two streams and --c5-join step: the half launched first")
     ap.add_argument("--c5-join", default="step", choices=("step", "phase"),
@@ -1026,7 +1029,37 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     fork = [torch.cuda.Event() for _ in range(2)]
     join = [torch.cuda.Event() for _ in range(2)]
 
+    # --c5-sets 2: ciphertext sets alternate; step k seals into cts[k % 2]
+    # and opens cts[(k + 1) % 2], sealed by step k - 1 (the same records
+    # and nonces, so the same bytes): the step's four launches are
+    # independent and run on four streams
+    cts = [ct, torch.empty_like(pt)] if args.c5_sets == 2 and side is not None else None
+    sides2 = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)] if cts else None
+    kstep = [0]
+    if cts:
+        for g in groups:
+            assert launch(g, False, inp=pt, out=cts[1]) == 0
+        torch.cuda.synchronize(dev)
+
     def step():
+        if cts:
+            k = kstep[0]
+            kstep[0] += 1
+            sealed, opened = cts[k % 2], cts[(k + 1) % 2]
+            fork[0].record(main_s)
+            for st_ in (side, *sides2):
+                st_.wait_event(fork[0])
+            rc = launch(groups[1], False, side.cuda_stream, inp=pt, out=sealed) \
+                or launch(groups[1], True, sides2[0].cuda_stream, inp=opened, out=back) \
+                or launch(groups[0], False, main_s.cuda_stream, inp=pt, out=sealed) \
+                or launch(groups[0], True, sides2[1].cuda_stream, inp=opened, out=back)
+            if rc:
+                raise RuntimeError(f"launch failed {rc:#x}")
+            for i, st_ in enumerate((side, *sides2)):
+                ev = join[0] if i == 0 else torch.cuda.Event()
+                ev.record(st_)
+                main_s.wait_event(ev)
+            return
         if side is not None and args.c5_join == "step":
             fork[0].record(main_s)
             side.wait_event(fork[0])
@@ -1083,6 +1116,8 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     elapsed = max_over_ranks(dist, torch, dev, timed(dist))
     if dist:
         dist.barrier()
+    if cts:  # verify the set the last timed step sealed
+        ct = cts[(kstep[0] - 1) % 2]
     # per-kernel times (separate, untimed pass) for the roofline line
     per = []
     for open_ in (False, True):
@@ -1149,6 +1184,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                    "states_per_gpu": S, "payload_bytes_per_step": int(2 * payload * world),
                    "streams": 2 if side is not None else 1,
                    "join": args.c5_join if side is not None else None,
+                   "sets": 2 if cts else 1,
                    "parallelism": f"states x{world}",
                    "settle": {"ms": args.settle_ms, "steps": settled[0], "s": round(settled[1], 3)}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -621,9 +621,13 @@ NA_DEV void seg_repair(const SegLane &q, const IO &io, uint32_t lane, uint32_t S
 /* A wave's job: every lane's segment q (key, nonce, pointers filled, blocks
    from seg_blocks) through seal or open; io initialised.  vf: verify-first
    open. */
-template <bool OPEN, bool PRIO, class IO>
+struct SegNoHook {
+    NA_DEV void operator()() const {}
+};
+
+template <bool OPEN, bool PRIO, class IO, class HOOK = SegNoHook>
 NA_DEV void seg_job(const SegLane &q, const uint32_t key[8], const IO &io, uint32_t lane, uint4 *tiles,
-                    uint8_t *status, bool vf, bool inplace, SegTL &tl)
+                    uint8_t *status, bool vf, bool inplace, SegTL &tl, const HOOK &after_pass = HOOK())
 {
     const uint32_t S = wave_max((q.nb + 1) / 2);
     const uint32_t kmax = wave_max(q.K);
@@ -635,6 +639,7 @@ NA_DEV void seg_job(const SegLane &q, const uint32_t key[8], const IO &io, uint3
     if (S) io.dma(lane, 0, tiles);
     if (!OPEN) {
         seg_pass<SEG_SEAL, PRIO>(q, io, lane, S, tiles, key, pre, r, rw, s, h, 0xffu, true, tl);
+        after_pass();
         const uint64_t tc = SegTL::now();
         const Fe acc = seg_combine(q, rw, h, kmax);
         if (q.live && q.k == 0) {
@@ -648,6 +653,7 @@ NA_DEV void seg_job(const SegLane &q, const uint32_t key[8], const IO &io, uint3
     }
     if (vf) seg_auth(q, io, lane, S, tiles, key, pre, r, rw, s, h);
     else seg_pass<SEG_OPEN1, PRIO>(q, io, lane, S, tiles, key, pre, r, rw, s, h, 0xffu, true, tl);
+    after_pass();
     const Fe acc = seg_combine(q, rw, h, kmax);
     bool okl = false;
     if (q.live && q.k == 0) {
@@ -853,7 +859,12 @@ NA_DEV SegLane seg_ragged_lane(const RaggedArgs &a, uint32_t e, uint32_t e0, uin
     return q;
 }
 
-/* Persistent: 2 workgroups per CU, each wave taking jobs from the ticket */
+/* Persistent: 2 workgroups per CU, each wave taking jobs from the ticket.
+   NA_SEG_PREFETCH (default 1): the next job's ticket and plan entries are
+   taken as the current job's data pass ends; 0: at the top of the loop. */
+#ifndef NA_SEG_PREFETCH
+#define NA_SEG_PREFETCH 1
+#endif
 template <bool OPEN>
 __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seg_ragged(RaggedArgs a, SegPlanHdr *p,
                                                                          const uint32_t *map)
@@ -870,30 +881,43 @@ __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seg_ragged(RaggedA
     const uint32_t n_jobs = p->n_jobs, total = p->total_lanes;
     SegTL tl;
     const uint64_t born = SegTL::now();
-    /* the next job's ticket and plan entries are taken while the current
-       job runs: a job's set-up was four dependent round trips (ticket, plan,
-       descriptor, key), 8-9 % of a wave's life (tools/seg_tl.py) */
-    uint32_t tk = 0;
-    if (lane == 0) tk = atomicAdd(&p->ticket, 1u);
-    uint32_t t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tk, 0, 64));
-    uint32_t e_nx, e0_nx;
-    seg_map_entries(map, total, n_jobs, t, lane, e_nx, e0_nx);
+    /* The next job's ticket and plan entries are taken as the current job's
+       data pass ends, so their round trips overlap its combine and tag (a
+       job's set-up was four dependent round trips: ticket, plan,
+       descriptor, key — 8-9 % of a wave's life, tools/seg_tl.py).  Taken
+       at the job's START instead, a busy wave held a reservation on the
+       next (long: longest first) job while free waves went on to shorter
+       ones: 10 % slower (profiles/r05/seg_prefetch_ab.txt). */
+    uint32_t t = 0, e_nx = 0, e0_nx = 0;
+    const auto next = [&]() {
+        uint32_t tn = 0;
+        if (lane == 0) tn = atomicAdd(&p->ticket, 1u);
+        t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tn, 0, 64));
+        seg_map_entries(map, total, n_jobs, t, lane, e_nx, e0_nx);
+    };
+#if NA_SEG_PREFETCH
+    next();
+#endif
     for (;;) {
         const uint64_t t0 = SegTL::now();
+#if !NA_SEG_PREFETCH
+        next();
+#endif
         if (t >= n_jobs) break; /* every wave draws one ticket past the end */
         const uint32_t e = e_nx, e0 = e0_nx;
-        if (lane == 0) tk = atomicAdd(&p->ticket, 1u);
         uint32_t key[8];
         SegLane q = seg_ragged_lane(a, e, e0, key);
-        t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tk, 0, 64));
-        seg_map_entries(map, total, n_jobs, t, lane, e_nx, e0_nx);
         seg_blocks(q);
         SegIOL io;
         io.tab = owners[w];
         io.init(q, lane);
         const bool inplace = q.src == q.dst;
         tl.add(1, SegTL::now() - t0);
+#if NA_SEG_PREFETCH
+        seg_job<OPEN, false>(q, key, io, lane, tiles[w], a.status, a.vf != 0, inplace, tl, next);
+#else
         seg_job<OPEN, false>(q, key, io, lane, tiles[w], a.status, a.vf != 0, inplace, tl);
+#endif
         const uint64_t td = SegTL::now();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the job's stores left before the tile is reused */
         __builtin_amdgcn_wave_barrier();
