@@ -205,17 +205,44 @@ NA_DEV void seg_store16(uint64_t a, const uint4 &q)
     __builtin_nontemporal_store(v, (seg_gvec *)(uintptr_t)a);
 }
 
+#ifndef NA_SEG_INTERIOR
+#define NA_SEG_INTERIOR 1
+#endif
 struct SegIOL {
     SegOwner *tab; /* this wave's 64 owners (LDS) */
+    /* wave-uniform: the smallest readable end and store limit over the
+       owners with blocks.  A step m >= 1 with 128 (m + 1) below them is
+       interior for every owner: no clamp, no limit test per instruction
+       (≈100 of a step's ≈2300 VALU, the owner-geometry arithmetic) */
+    uint32_t min_hi, min_sl;
     NA_DEV void init(const SegLane &q, uint32_t lane)
     {
-        tab[lane] = seg_geom(q);
+        const SegOwner g = seg_geom(q);
+        tab[lane] = g;
+        uint32_t h = g.hi ? g.hi : 0xffffffffu, sl = g.hi ? (g.sl & 0x7fffffffu) : 0xffffffffu;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            h = min(h, (uint32_t)__shfl_xor((int)h, off, 64));
+            sl = min(sl, (uint32_t)__shfl_xor((int)sl, off, 64));
+        }
+        min_hi = __builtin_amdgcn_readfirstlane(h);
+        min_sl = __builtin_amdgcn_readfirstlane(sl);
         __builtin_amdgcn_wave_barrier();
     }
     NA_DEV void dma(uint32_t lane, uint32_t m, uint4 *t) const
     {
         const uint32_t c = solo_chunk(lane);
         const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)t);
+        if (NA_SEG_INTERIOR && m >= 1 && 128u * m + 128u <= min_hi) { /* interior step (wave-uniform) */
+            const uint32_t off = 128u * m + 16u * c;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const SegOwner &o = tab[8 * i + (lane >> 3)];
+                const uint64_t ga = o.in + off;
+                if (o.hi && SEG_OK(ga, 16, 1, m << 16 | lane << 8 | i)) dma16_asm((const void *)(uintptr_t)ga, base + 1024u * (uint32_t)i);
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const SegOwner &o = tab[8 * i + (lane >> 3)];
@@ -229,6 +256,7 @@ struct SegIOL {
         /* the tile values and owner entries first, one wait, then the stores
            (a read and its wait inside each store's branch serialised them) */
         const uint32_t off = 128u * m + 16u * solo_chunk(lane);
+        const bool interior = NA_SEG_INTERIOR && m >= 1 && 128u * m + 128u <= min_sl; /* wave-uniform */
         uint4 v[8];
         uint64_t dst[8];
         uint32_t ok = 0;
@@ -237,7 +265,7 @@ struct SegIOL {
             const SegOwner &o = tab[8 * i + (lane >> 3)];
             v[i] = t[64 * i + lane];
             dst[i] = o.out + off;
-            ok |= (o.hi && seg_store_ok(off, o.sl) ? 1u : 0u) << i;
+            ok |= (o.hi && (interior || seg_store_ok(off, o.sl)) ? 1u : 0u) << i;
         }
         ok &= okm;
 #pragma unroll
