@@ -988,12 +988,15 @@ void worker_note_ctx(Worker &w, const void *h)
 void worker_abandon(Worker &w, uint32_t k)
 {
     WorkerGroup &g = *w.g;
-    std::lock_guard<std::mutex> gl(g.mu);
+    /* the stop words and this slot's header first, without the group's
+       lock: a caller holding it may be waiting in group_launch for this very
+       group to leave */
     set_stops(g, 1u);
     const uint32_t bad = k ^ 0x80000000u;
     const __m128i c = w.vram ? _mm_set_epi32(0, (int)bad, 0, (int)bad) : _mm_set_epi32(0, 0, 0, (int)bad);
     _mm_store_si128((__m128i *)w.req, c);
     _mm_sfence();
+    std::lock_guard<std::mutex> gl(g.mu);
     g.abandoned |= 1u << (int)(&w - g.slot);
     g.state = -2;
 }
