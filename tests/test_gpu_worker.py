@@ -222,3 +222,15 @@ def test_free_beside_concurrent_caller_parks_only_that_worker(gpu):
                        text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "parked_ok 1" in r.stdout
+
+
+def test_group_stays_while_one_slot_is_busy(gpu):
+    """Worker groups (round 5): a group's workgroup leaves for idleness only
+    when every slot of the group has been idle, so one thread's idle slot
+    does not relaunch the group another thread keeps busy; with both quiet
+    the group leaves by itself (tests/worker_mode_check.py --group-idle)."""
+    env = {"NOISE_AEAD_WORKER_QUEUES": "1", "NOISE_AEAD_WORKER_SLOTS": "2", "NOISE_AEAD_DEBUG_WORKER_IDLE_MS": "20"}
+    r = subprocess.run([sys.executable, "-u", os.path.join(os.path.dirname(__file__), "worker_mode_check.py"),
+                        "--group-idle"], env=dict(os.environ, **env), timeout=110, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "group_idle_ok 1" in r.stdout

@@ -155,7 +155,58 @@ def free_concurrent():
     return 0 if ok else 1
 
 
+def group_idle():
+    """--group-idle (run with NOISE_AEAD_WORKER_QUEUES=1,
+    NOISE_AEAD_WORKER_SLOTS=2, NOISE_AEAD_DEBUG_WORKER_IDLE_MS=20): one
+    group of two slots.  The main thread makes one call (its slot then stays
+    idle) while thread A keeps calling for 300 ms: the group must not leave
+    for the idle slot's sake (a workgroup leaves for idleness only when every
+    slot of its group is idle), so no relaunch happens; once both are quiet
+    the group leaves by itself.  Prints "group_idle_ok 1"."""
+    import threading
+    import time
+    lib = aead.lib()
+    lib.noise_aead_debug_workers_resident.restype = int
+    lib.noise_aead_debug_worker_launches.restype = int
+    _, mine = aead.CipherState.new_by_id(0x4301)
+    mine.init_key(bytes(range(32)))
+    started = threading.Event()
+    stop = [False]
+    errs = []
+
+    def caller():
+        _, cs = aead.CipherState.new_by_id(0x4301)
+        cs.init_key(bytes(range(3, 35)))
+        started.set()
+        while not stop[0]:
+            if len(cs.seal(bytes(1400))) != 1416:
+                errs.append("seal")
+        cs.free()
+
+    assert len(mine.seal(bytes(100))) == 116  # slot 0: launches the group
+    th = threading.Thread(target=caller)
+    th.start()
+    started.wait(30)
+    time.sleep(0.05)
+    l0 = lib.noise_aead_debug_worker_launches()
+    time.sleep(0.3)  # 15 idle timeouts of the main thread's slot
+    l1 = lib.noise_aead_debug_worker_launches()
+    stop[0] = True
+    th.join()
+    t0 = time.time()
+    while lib.noise_aead_debug_workers_resident() and time.time() - t0 < 2.0:
+        time.sleep(0.005)
+    left = lib.noise_aead_debug_workers_resident() == 0
+    mine.free()
+    ok = l0 == l1 and left and not errs
+    print("launches", l0, l1, "left", left, "errs", errs[:3])
+    print("group_idle_ok", 1 if ok else 0)
+    return 0 if ok else 1
+
+
 if __name__ == "__main__":
+    if "--group-idle" in sys.argv:
+        sys.exit(group_idle())
     if "--free-check" in sys.argv:
         sys.exit(free_check())
     if "--free-concurrent" in sys.argv:
