@@ -319,6 +319,24 @@ def issue_bound(pmc, avg_launch_ms):
             "source": "SQ_INSTS_VALU from the committed PMC profile / live launch time"}
 
 
+# The stream rank 0's one JSON line goes to.  A run with a process group
+# points file descriptor 1 at stderr (keep_stdout_for_line): RCCL prints its
+# version banner on stdout when a communicator is made, and the line must be
+# the only thing there.
+LINE_OUT = None  # None: sys.stdout as it is at the time of the line
+
+
+def keep_stdout_for_line():
+    global LINE_OUT
+    sys.stdout.flush()
+    LINE_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
+def emit_line(result):
+    print(json.dumps(result), file=LINE_OUT or sys.stdout, flush=True)
+
+
 def launch_ranks(n: int) -> int:
     """`--gpus N` (N > 1) without a launcher: run this script as N ranks of a
     child torch.distributed.run on 127.0.0.1 and return its exit status.  The
@@ -340,6 +358,10 @@ def launch_ranks(n: int) -> int:
         else:
             sys.stderr.write(line)
     return proc.wait()
+
+
+# C5's two streams when made before the process group (main)
+C5_STREAMS = []
 
 
 def init_dist(world, local, dry_run):
@@ -378,7 +400,7 @@ def dry_run(args, rank, world):
               "dry_run": True, "rank_env": {"WORLD_SIZE": os.environ.get("WORLD_SIZE"),
                                              "MASTER_ADDR": os.environ.get("MASTER_ADDR")}}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit_line(result)
     if dist:
         dist.destroy_process_group()
 
@@ -448,6 +470,10 @@ def parse_args():
     ap.add_argument("--c5-join", default="step", choices=("step", "phase"),
                     help="C5 with two streams: each cipher's open follows its own seal and the halves "
                          "join once per step (step), or both seals finish before either open (phase)")
+    ap.add_argument("--rccl", action="store_true",
+                    help="form the nccl (RCCL) process group and run the scatter/seal/gather leg and the "
+                         "max-over-ranks timing through it even at WORLD_SIZE=1 (a one-GPU check of the "
+                         "N > 1 code path on RCCL; the value is the N = 1 value)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / process-group plumbing only, no GPU work (CPU tests)")
     return ap.parse_args()
@@ -459,11 +485,20 @@ def main():
     if env_world is None and (args.gpus or 1) > 1:
         sys.exit(launch_ranks(args.gpus))
     world = int(env_world or 1)
+    if args.rccl and env_world is None:  # a one-rank group without a launcher
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        os.environ.update(RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port))
     if args.gpus is not None and args.gpus != world:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 or args.rccl:
+        keep_stdout_for_line()
     if args.dry_run:
         return dry_run(args, rank, world)
 
@@ -473,8 +508,21 @@ def main():
     dist = None
     if REHEARSE:
         local = 0
-    if world > 1:
+    if world > 1 or args.rccl:
         torch.cuda.set_device(local)
+        if args.config == "c5" and args.c5_streams == 2:
+            # HIP binds a stream to one of the process's GPU_MAX_HW_QUEUES (4)
+            # hardware queues at the stream's first use.  First used after
+            # RCCL's streams, C5's two streams shared one queue and the halves
+            # ran one after the other (step 2.09 -> 2.43 ms; the kernel trace's
+            # Queue_Id, profiles/r05/rccl_one_rank.txt); used once here, before
+            # the process group, they own two queues
+            C5_STREAMS[:] = [torch.cuda.Stream(torch.device("cuda", local)) for _ in range(2)]
+            for st_ in C5_STREAMS:
+                with torch.cuda.stream(st_):
+                    torch.zeros(1, device=torch.device("cuda", local)).add_(1)
+            torch.cuda.synchronize()
+            torch.cuda.set_stream(C5_STREAMS[0])
         dist = init_dist(world, local, False)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -571,7 +619,7 @@ def main():
     if verify is not None:
         result["verified"] = verify.pop("ok")
         result["verify"] = verify
-    if world > 1 and not args.no_xfer:
+    if dist is not None and not args.no_xfer:
         try:  # reported beside the value; a failure here never voids the bench line
             result["scatter_gather"] = xfer_leg(args, torch, dist, dev, A, rank, world, N, L,
                                                 wl.in_stride, wl.out_stride, wl.sh, wl.sets, wl.seal)
@@ -881,6 +929,8 @@ def finish(args, result, rank, world, dist):
         result["n1_value"] = n1
         result["n1_source"] = ("--n1-value" if args.n1_value else
                                "in-run: rank 0 alone on the same per-GPU work, other ranks at a barrier")
+    if dist is not None:
+        result["process_group"] = {"backend": str(dist.get_backend()), "world_size": dist.get_world_size()}
     if REHEARSE and world > 1:
         # every rank on one GPU, collectives on gloo: exercises the N > 1 code
         # path only; per-kernel rates of ranks sharing a GPU mean nothing
@@ -888,7 +938,7 @@ def finish(args, result, rank, world, dist):
         result["rehearsal"] = (f"{world} ranks on ONE GPU, gloo process group (collectives via host "
                                "memory): a code-path rehearsal, not a multi-GPU measurement")
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit_line(result)
     if dist:
         dist.destroy_process_group()
 
@@ -1023,7 +1073,8 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     # join at the end of the step.  phase: both seals finish before either
     # open (round 4's shape).
     main_s = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(dev, priority=-1 if args.c5_prio == "aes" else 0) \
+    side = (C5_STREAMS[1] if C5_STREAMS and args.c5_prio != "aes" else
+            torch.cuda.Stream(dev, priority=-1 if args.c5_prio == "aes" else 0)) \
         if args.c5_streams == 2 and len(groups) == 2 else None  # the AES-GCM half
     cha_s = torch.cuda.Stream(dev, priority=-1) if side is not None and args.c5_prio == "chacha" else None
     fork = [torch.cuda.Event() for _ in range(2)]
@@ -1201,7 +1252,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
     if verify is not None:
         result["verified"] = verify.pop("ok")
         result["verify"] = verify
-    if world > 1 and not args.no_xfer:
+    if dist is not None and not args.no_xfer:
         try:  # reported beside the value; a failure here never voids the bench line
             result["scatter_gather"] = xfer_leg_mixed(args, torch, dist, dev, A, rank, world, R, S,
                                                       lay, pt, groups, launch)

@@ -137,3 +137,16 @@ def test_bench_module_constants_exist():
     assert names, "no constants found"
     missing = sorted(n for n in names if not hasattr(A, n))
     assert not missing, missing
+
+
+def test_group_runs_keep_stdout_for_the_line():
+    """A run with a process group points fd 1 at stderr (RCCL prints its
+    banner on stdout when a communicator is made); the JSON line still goes
+    to the original stdout, alone."""
+    import subprocess
+    code = ("import os, sys; sys.path.insert(0, %r); import bench; bench.keep_stdout_for_line(); "
+            "os.write(1, b'RCCL version : x\\n'); print('stray'); bench.emit_line({'metric': 'm'})" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"metric": "m"}']
+    assert "RCCL version" in r.stderr and "stray" in r.stderr
