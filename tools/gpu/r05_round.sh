@@ -1,7 +1,7 @@
 # Round-5 measurement set on the final code: all GPU tests, smoke(), every
 # bench line at the driver's --steps 20 --warmup 5 (C2 default and C4 with
 # their CPU baselines, C3, C5, perf), the verify-first open order's C2/C3
-# lines, worker latency and thread scaling, end-to-end host paths.
+# lines, the one-rank RCCL lines (--rccl), worker latency and thread scaling, end-to-end host paths.
 # Outputs in gpurun_out/r05_round/.  PART=1: tests, smoke, bench lines;
 # PART=2: latency, thread scaling, host paths (unset: both).
 set -eu
@@ -27,6 +27,8 @@ b perf --config perf --steps 20 --warmup 5
 b c2_verify_first --steps 20 --warmup 5 --verify-first --no-cpu-baseline
 b c3_verify_first --config c3 --steps 20 --warmup 5 --verify-first --no-cpu-baseline
 b c5_verify_first --config c5 --steps 10 --warmup 2 --verify-first --no-cpu-baseline
+b c2_rccl --steps 20 --warmup 5 --rccl --no-cpu-baseline
+b c5_rccl --config c5 --steps 20 --warmup 5 --rccl --no-cpu-baseline
 timeout -k 10 300 python bench.py > $O/bench_default_noflags.json 2> $O/bench_default_noflags.err || { tail -20 $O/bench_default_noflags.err; exit 1; }
 fi
 if [ "${PART:-2}" = 2 ]; then
