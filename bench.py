@@ -541,7 +541,8 @@ def main():
     if dist:
         dist.barrier()
     # verify first: the per-direction pass below seals and opens the sets again
-    verify = None if args.no_verify else wl.verify(args.config, rank, world)
+    verify = verify_over_ranks(dist, torch, dev,
+                               None if args.no_verify else wl.verify(args.config, rank, world))
     seal_ms, open_ms = wl.per_direction_ms()
 
     L, AD = wl.L, wl.AD
@@ -918,6 +919,26 @@ def n1_reference(args, cfg, A, torch, dev, rank, dist, wl, N, S, world):
     return round(v, 2)
 
 
+def verify_over_ranks(dist, torch, dev, verify):
+    """Every rank checks its own shard (statuses, round trip, the golden
+    digest of its set-0 output); with a process group the line's `verified`
+    is all ranks' verdict and `verify.ranks` lists each rank's (ok, digest:
+    1 match, 0 no golden for that rank/layout, -1 MISMATCH)."""
+    if dist is None or verify is None:
+        return verify
+    d = verify.get("sealed_digest_set0", verify.get("sealed_digest"))
+    code = 1 if d == "match" else -1 if d == "MISMATCH" else 0
+    mine = cpu_if_rehearsal(torch.tensor([1 if verify["ok"] else 0, code], dtype=torch.int64, device=dev))
+    got = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(got, mine)
+    ranks = [{"ok": bool(g[0].item()), "digest": {1: "match", 0: "no golden", -1: "MISMATCH"}[int(g[1].item())]}
+             for g in got]
+    verify["rank0_ok"] = verify["ok"]
+    verify["ok"] = all(r["ok"] for r in ranks)
+    verify["ranks"] = ranks
+    return verify
+
+
 def finish(args, result, rank, world, dist):
     """Per-GPU efficiency when an N = 1 value is given, the
     rehearsal label, then rank 0 prints the one JSON line."""
@@ -1207,6 +1228,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
             del ct_h
         verify = {"ok": ok and rt_ok and digest != "MISMATCH", "statuses_zero": ok, "round_trip": rt_ok,
                   "sealed_digest": digest, "golden": "tests/golden/shard_digests.json"}
+    verify = verify_over_ranks(dist, torch, dev, verify)
     payload = sum(g["bytes"] for g in groups)
     value = 2.0 * payload * world * args.steps / elapsed / GIB
     ms, g, open_ = max(per, key=lambda x: x[0])

@@ -25,15 +25,20 @@ def _port():
         return so.getsockname()[1]
 
 
-def _run(config, extra=()):
+def _run(config, extra=(), rehearse_ranks=0):
     e = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         e.pop(k, None)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--rccl", "--config", config,
-           "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--no-cpu-baseline",
-           "--xfer-reps", "2", *extra]
+    common = ["--config", config, "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--no-cpu-baseline",
+              "--xfer-reps", "2", *extra]
+    if rehearse_ranks:  # bench.py starts its own ranks, all on this GPU, gloo
+        e["NOISE_BENCH_REHEARSE"] = "1"
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(rehearse_ranks), "--no-n1"]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+               os.path.join(ROOT, "bench.py"), "--gpus", "1", "--rccl"]
+    cmd += common
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=e, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     # stdout holds the one line only: RCCL's banner goes to stderr
@@ -49,6 +54,21 @@ def _check(d):
     sg = d["scatter_gather"]
     assert "error" not in sg, sg
     assert "nccl" in sg["collective"]
+    assert d["scatter_gather_ok"] is True
+    assert [r["digest"] for r in d["verify"]["ranks"]] == ["match"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["c2", "c5"])
+def test_two_rank_rehearsal_verifies_every_shard(config):
+    """NOISE_BENCH_REHEARSE=1 --gpus 2: two ranks on this GPU over gloo, each
+    sealing its own shard; the line's `verified` is both ranks' verdict, and
+    each rank's set-0 output matches its golden shard digest
+    (tests/golden/shard_digests.json, N = 2)."""
+    d = _run(config, rehearse_ranks=2)
+    assert d["n_gpus"] == 2 and "rehearsal" in d
+    assert d["verified"] is True
+    assert [r["digest"] for r in d["verify"]["ranks"]] == ["match", "match"]
     assert d["scatter_gather_ok"] is True
 
 
