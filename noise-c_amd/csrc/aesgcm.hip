@@ -1466,7 +1466,7 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
         rv.nonce = d.nonce;
         rv.len = d.len;
         rv.ad_len = d.ad_len;
-        bool ok;
+        bool ok = false; /* every path below sets it */
         const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
         const bool vf = OPEN && a.vf;
         bool done = false;

@@ -1408,6 +1408,55 @@ NA_DEV void solo_auth(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
     }
 }
 
+/* The verify-first open's DEC pass from the last step back to the first
+   (NA_DEC_REV): key-stream blocks are independent of each other, and the
+   AUTH pass leaves steps S-1 and S-2 in the two tiles (it refills a tile
+   with step m+2 only while m+2 < S), so those two are decrypted without
+   reading them again and the pass starts without a DMA wait.  Otherwise
+   solo_pass<SOLO_DEC> with the step order reversed: the wait, the read of
+   step m, the store of step m+1's output from the other tile, the DMA of
+   step m-1 into it, the key stream into this tile.  C2 --verify-first
+   1396-1431 -> 1460-1468 GiB/s, three interleaved rounds
+   (profiles/r05/dec_rev_ab.txt); the last steps read by the AUTH pass are
+   also the likeliest still in L2.  NA_DEC_REV=0: the forward pass (A/B). */
+#ifndef NA_DEC_REV
+#define NA_DEC_REV 1
+#endif
+#if NA_DEC_REV
+NA_DEV void solo_dec_rev(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const uint32_t key[8],
+                         const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, uint32_t okm, bool ok)
+{
+    for (uint32_t k = 0; k < q.S; ++k) {
+        const uint32_t m = q.S - 1 - k;
+        uint4 *cur = tiles + SOLO_TILE * (m & 1), *nxt = tiles + SOLO_TILE * ((m + 1) & 1);
+        uint32_t wu[2][16];
+        solo_wait();
+        solo_get(cur, q.lane, 0, wu[0]);
+        solo_get(cur, q.lane, 1, wu[1]);
+        if (k >= 1) solo_store(a, q.rec0, q.lane, m + 1, q.full_lim, nxt, okm);
+        __builtin_amdgcn_wave_barrier();
+        if (k >= 1 && m >= 1) solo_dma(a, q.rec0, q.lane, m - 1, q.lim, nxt); /* k = 0: step S-2 is there */
+        prio_by_progress(k, q.S);
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t j = 2 * m + u;
+            if (j < q.J) {
+                uint32_t x[16], w[16];
+                chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) w[i] = wu[u][i] ^ x[i];
+                if (j == q.J - 1 && q.live && ok) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
+                solo_put(cur, q.lane, u, w);
+            }
+        }
+    }
+    if (q.S) {
+        __builtin_amdgcn_wave_barrier();
+        solo_store(a, q.rec0, q.lane, 0, q.full_lim, tiles, okm);
+    }
+}
+#endif
+
 /* The AUTH pass with the ciphertext loaded straight into registers instead
    of through the LDS tiles: each lane reads its own record's 128-B step with
    eight 16-B loads (whole 128-B lines), D steps in flight (D x 32 VGPRs,
@@ -1522,8 +1571,12 @@ NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
         for (int i = 0; i < 8; ++i)
             okm |= (__shfl((int)ok, (int)(8u * i + (lane >> 3)), 64) != 0 ? 1u : 0u) << i;
         __builtin_amdgcn_wave_barrier(); /* the AUTH pass's tile reads are done */
+#if NA_DEC_REV && !NA_AUTH_REG
+        solo_dec_rev(a, q, tiles, key, pre, n_lo, n_hi, okm, ok);
+#else
         if (S) solo_dma(a, rec0, lane, 0, lim, tiles);
         solo_pass<SOLO_DEC>(a, q, tiles, key, pre, n_lo, n_hi, r, h, okm, ok);
+#endif
         return;
     }
     const bool bad = live && !ok;
