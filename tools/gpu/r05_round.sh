@@ -8,7 +8,7 @@ set -eu
 R=$GRAFT_REPO_ROOT; cd $R
 O=$R/gpurun_out/${ROUND_DIR:-r05_round}; mkdir -p $O
 if [ -z "${SKIP_TESTS:-}" ] && [ "${PART:-1}" = 1 ]; then
-timeout -k 10 900 python -u -m pytest tests/ -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/ -m gpu -v -x --durations=10 --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
