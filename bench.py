@@ -61,10 +61,17 @@ CONFIGS = {
                  workload="ChaCha20-Poly1305 64Ki x 1024B records + 32B AD (tests/performance shape)"),
     # C5 per GPU = 1/8 of the 8-GPU job (1 Mi records, 4096 states in total):
     # lengths 64 + splitmix64(seed_len + i) mod 16321, cipher by state parity.
-    "c5": dict(cipher=None, records=131072, len=None, states=512,
+    "c5": dict(cipher=None, records=131072, len=None, states=512, mixed=True,
                workload="Mixed ChaChaPoly (even states) + AESGCM (odd states), 64 B-16 KiB "
                         "records (SURVEY.md 8d C5), 128 Ki records / 512 CipherStates per GPU, "
                         "ragged descriptors"),
+    # C5's layout rule at 1/8 of its records per GPU (256 records per state as
+    # in C5): the multi-rank rehearsal of the ragged path in the GPU tests
+    # (tests/test_gpu_rccl.py), with its own golden shard digests.  Not a
+    # bench line.
+    "c5s": dict(cipher=None, records=16384, len=None, states=64, mixed=True,
+                workload="C5's mixed ChaChaPoly + AESGCM 64 B-16 KiB layout, reduced to 16 Ki records / "
+                         "64 CipherStates per GPU (multi-rank rehearsal)"),
 }
 SEED_LEN, SEED_PT, SEED_KEY = 0x6C656E, 0x7074, 0x6B6579
 # NOISE_BENCH_REHEARSE=1: rehearse the N>1 code path on a one-GPU box — every
@@ -446,9 +453,11 @@ def parse_args():
                     help="N > 1: skip the in-run N = 1 reference (rank 0 alone) behind per_gpu_efficiency")
     ap.add_argument("--n1-value", type=float, default=None,
                     help="N = 1 value of the same config from another run (overrides the in-run one)")
-    ap.add_argument("--mode", default="duplex", choices=("duplex", "separate"),
+    ap.add_argument("--mode", default="duplex", choices=("duplex", "separate", "seal"),
                     help="duplex: each step seals one set and opens another in ONE launch "
-                         "(noise_aead_dev_duplex_uniform); separate: a seal launch then an open launch")
+                         "(noise_aead_dev_duplex_uniform); separate: a seal launch then an open launch; "
+                         "seal: encrypt only, one standalone seal launch per step (the north star's "
+                         "literal metric: device-resident ChaCha20-Poly1305 encrypt, C2-C4/perf)")
     ap.add_argument("--events", default="ends", choices=("ends", "step"),
                     help="ends: HIP events only around the timed region (per-launch time = "
                          "its interval / launches); step: events at every launch boundary")
@@ -457,7 +466,11 @@ def parse_args():
     ap.add_argument("--ct-ghash", action="store_true",
                     help="AES-GCM: NOISE_AEAD_FLAG_CT_GHASH (table-free GHASH)")
     ap.add_argument("--verify-first", action="store_true",
-                    help="opens with NOISE_AEAD_FLAG_VERIFY_FIRST (authenticate, then decrypt)")
+                    help="opens with NOISE_AEAD_FLAG_VERIFY_FIRST (authenticate, then decrypt): the "
+                         "default open order since round 6, kept as an explicit no-op")
+    ap.add_argument("--one-pass", action="store_true",
+                    help="ChaChaPoly opens with the opt-in NOISE_AEAD_FLAG_ONE_PASS (decrypt while "
+                         "authenticating; a rejected record's plaintext is undone before the kernel ends)")
     ap.add_argument("--c5-streams", type=int, default=2, choices=(1, 2),
                     help="C5: 2 = the AES-GCM and ChaChaPoly halves on two streams, concurrently")
     ap.add_argument("--c5-prio", default="none", choices=("none", "aes", "chacha"),
@@ -510,7 +523,7 @@ def main():
         local = 0
     if world > 1 or args.rccl:
         torch.cuda.set_device(local)
-        if args.config == "c5" and args.c5_streams == 2:
+        if CONFIGS[args.config].get("mixed") and args.c5_streams == 2:
             # HIP binds a stream to one of the process's GPU_MAX_HW_QUEUES (4)
             # hardware queues at the stream's first use.  First used after
             # RCCL's streams, C5's two streams shared one queue and the halves
@@ -528,7 +541,7 @@ def main():
     torch.cuda.set_device(dev)
 
     cfg = CONFIGS[args.config]
-    if args.config == "c5":
+    if cfg.get("mixed"):
         return run_mixed(args, cfg, A, torch, dev, rank, world, dist)
     N, S = cfg["records"], cfg["states"]
     if cfg.get("strong"):
@@ -537,16 +550,19 @@ def main():
         N, S = N // world, S // world
     wl = UniformWork(args, cfg, A, torch, dev, N, S, shard(N, S, rank, world))
     elapsed = wl.timed(args.steps, args.warmup, dist)
+    # the per-direction pass right after the timed region, at the clock it
+    # left (it used to follow verify()'s D2H and SHA-256,
+    # an idle GPU); its outputs go to scratch buffers, so what verify()
+    # checks is still only what the timed launches wrote
+    seal_ms, open_ms = wl.per_direction_ms()
     elapsed = max_over_ranks(dist, torch, dev, elapsed)
     if dist:
         dist.barrier()
-    # verify first: the per-direction pass below seals and opens the sets again
     verify = verify_over_ranks(dist, torch, dev,
                                None if args.no_verify else wl.verify(args.config, rank, world))
-    seal_ms, open_ms = wl.per_direction_ms()
 
     L, AD = wl.L, wl.AD
-    payload_step = 2.0 * N * L * world                         # both directions, all ranks
+    payload_step = wl.dirs * N * L * world                     # both directions (seal mode: one), all ranks
     value = payload_step * args.steps / elapsed / GIB
     alg_seal = N * (2 * L + 16 + AD) + len(wl.sh["key_ids"]) * 40  # SURVEY §8d algorithmic bytes (+AD read)
     # a VERIFY_FIRST open shares the duplex launch only with the one-lane
@@ -555,7 +571,7 @@ def main():
     vf_duplex = "_duplex_" in kernel_name(wl.cipher, N, wl.sh["rps"], wl.lanes, wl.in_stride,
                                           wl.out_stride, L, True, args.ct_ghash) and \
         (wl.cipher == AES or wl.lanes == 1)
-    two_launch = wl.duplex and args.verify_first and not vf_duplex
+    two_launch = wl.duplex and wl.vf and not vf_duplex
     kname = kernel_name(wl.cipher, N, wl.sh["rps"], wl.lanes, wl.in_stride, wl.out_stride, L,
                         wl.duplex and not two_launch, args.ct_ghash)
     if two_launch:
@@ -569,17 +585,20 @@ def main():
     else:
         alg_launch, launch_ms_ = alg_seal, seal_ms
     achieved = alg_launch / (launch_ms_ * 1e-3) / 1e9
-    # the committed PMC profiles are of the default open order (ChaChaPoly:
-    # one pass; AES-GCM opens always verify first)
-    pmc = {} if args.verify_first and wl.cipher != AES else \
-        load_pmc(args.config, kname, 1.0 / world if cfg.get("strong") else 1.0)
+    # the committed PMC profiles are of the default open order (verify
+    # first since round 6; profiles/traffic_<cfg>.json), of the standalone
+    # seal for --mode seal (traffic_<cfg>_seal.json)
+    pmc = {} if args.one_pass and wl.cipher != AES else \
+        load_pmc(args.config + ("_seal" if wl.seal_only else ""), kname,
+                 1.0 / world if cfg.get("strong") else 1.0)
     traffic = pmc.get("hbm_bytes_per_launch")
     S_all = S * world
+    op = "encrypt" if wl.seal_only else "encrypt+decrypt"
     result = {
-        "metric": (f"GiB/s device-resident AEAD encrypt+decrypt, {N * world // 1024}Ki x {L}B "
+        "metric": (f"GiB/s device-resident AEAD {op}, {N * world // 1024}Ki x {L}B "
                    f"records in total over {S_all} CipherStates, sharded by state"
                    if cfg.get("strong") else
-                   f"GiB/s device-resident AEAD encrypt+decrypt, {N // 1024}Ki x {L}B records"
+                   f"GiB/s device-resident AEAD {op}, {N // 1024}Ki x {L}B records"
                    + (f" + {AD}B AD" if AD else "") + " per GPU"),
         "value": round(value, 2),
         "unit": "GiB/s",
@@ -600,12 +619,13 @@ def main():
                    "open_reads_set_sealed_steps_before": wl.lag,
                    "settle": {"ms": args.settle_ms, "steps": wl.settle_steps,
                               "s": round(wl.settle_s, 3)},
-                   "open_order": ("verify-first (NOISE_AEAD_FLAG_VERIFY_FIRST: authenticate, then "
-                                  "decrypt verified records)" if args.verify_first else
-                                  "verify-first (every AES-GCM open: authenticate, then decrypt "
-                                  "verified records)" if wl.cipher == AES else
-                                  "one pass (decrypt while authenticating; a rejected record's "
-                                  "plaintext is undone before the kernel ends)"),
+                   "open_order": ("verify-first (the default: authenticate, then decrypt verified "
+                                  "records; cipher-chachapoly.c:135-141, cipher-aesgcm.c:172-188)"
+                                  if wl.vf else
+                                  "one pass (NOISE_AEAD_FLAG_ONE_PASS: decrypt while authenticating; "
+                                  "a rejected record's plaintext is undone before the kernel ends)"),
+                   "per_direction": "seal_gibs / open_gibs: 20 standalone launches each, right after "
+                                    "the timed region (settled clock), outputs to scratch buffers",
                    **({"ct_ghash": True} if args.ct_ghash else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -708,7 +728,10 @@ class UniformWork:
             self.sets.append((pt, ct, back, st))
         torch.cuda.synchronize(dev)
         self.sflags = A.FLAG_CT_GHASH if args.ct_ghash else 0
-        self.oflags = self.sflags | (A.FLAG_VERIFY_FIRST if args.verify_first else 0)
+        # open order: verify first (the library's default since round 6; AES-GCM
+        # always), or the opt-in one pass for ChaChaPoly
+        self.vf = not args.one_pass or cipher == AES
+        self.oflags = self.sflags | (A.FLAG_ONE_PASS if args.one_pass else 0)
         # Each step seals set b = s % sets and opens set (s - LAG) % sets, sealed
         # LAG steps earlier: the ciphertext an open reads was written two full
         # steps (> 700 MB of traffic) before, so it comes from HBM, not from the
@@ -716,6 +739,9 @@ class UniformWork:
         # every open has ciphertext; a set's ciphertext is the same at every seal.
         self.lag = 2 if args.sets >= 3 else 0
         self.duplex = args.mode == "duplex"
+        # --mode seal: encrypt only, one standalone seal launch per step
+        self.seal_only = args.mode == "seal"
+        self.dirs = 1 if self.seal_only else 2
         # lanes 0 in the jobs: the library's own choice, which differs
         # between a duplex launch and standalone seals/opens; self.lanes is
         # the duplex (timed) launch's, for the kernel names
@@ -773,6 +799,8 @@ class UniformWork:
         b, bo = w % self.args.sets, (w - self.lag) % self.args.sets
         if self.duplex:
             assert self.step_duplex(b, bo) == 0
+        elif self.seal_only:
+            assert self.seal(b) == 0
         else:
             assert self.seal(b) == 0
             assert self.open_(bo) == 0
@@ -815,6 +843,8 @@ class UniformWork:
             if self.duplex or not per_step:
                 if self.duplex:
                     rc = self.step_duplex(b, bo, self.streams[s % len(self.streams)].cuda_stream)
+                elif self.seal_only:
+                    rc = self.seal(b, stream=self.streams[s % len(self.streams)].cuda_stream)
                 else:
                     st_ = self.streams[s % len(self.streams)].cuda_stream
                     rc = self.seal(b, stream=st_) or self.open_(bo, stream=st_)
@@ -841,33 +871,51 @@ class UniformWork:
             # from the end of step 1 on: the first step also carries the
             # host's submission of the first launch after ev[0] (~3 us per
             # step at K = 20), which is no kernel time
+            per = 1 if (self.duplex or self.seal_only) else 2  # launches per step
             if steps > 1:
-                self.launch_ms = ev[1].elapsed_time(ev[steps]) / (steps - 1) / (1 if self.duplex else 2)
+                self.launch_ms = ev[1].elapsed_time(ev[steps]) / (steps - 1) / per
             else:
-                self.launch_ms = ev[0].elapsed_time(ev[steps]) / steps / (1 if self.duplex else 2)
+                self.launch_ms = ev[0].elapsed_time(ev[steps]) / steps / per
         else:
             self.launch_ms = None
         return elapsed
 
     def per_direction_ms(self):
         """Seal / open launch times: per-step events, or (duplex, ends, two
-        streams) a separate serial, untimed pass of the two kernels."""
-        torch, steps = self.torch, self.args.steps
-        if not (self.duplex or not self.per_step or len(self.streams) > 1):
+        streams, seal mode) a separate serial pass of the two kernels, run
+        right after the timed region (the settled clock) into scratch outputs:
+        the sets' sealed records and opened outputs stay those of the timed
+        launches, which verify() checks.  The opens read the sets' sealed
+        records (every set is sealed before timing)."""
+        torch, steps, A = self.torch, self.args.steps, self.A
+        if not (self.duplex or not self.per_step or len(self.streams) > 1 or self.seal_only):
             seal_ms = sum(e[0].elapsed_time(e[1]) for e in self.ev) / steps
             open_ms = sum(e[1].elapsed_time(e[2]) for e in self.ev) / steps
             return seal_ms, open_ms
+        N = self.N
+        ct_s = torch.empty(N * self.out_stride, dtype=torch.uint8, device=self.dev)
+        back_s = torch.empty(N * self.in_stride, dtype=torch.uint8, device=self.dev)
+        st_s = torch.empty(N, dtype=torch.uint8, device=self.dev)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         reps, sets = 20, self.args.sets
         e[0].record(self.stream)
-        for r in range(reps):
-            self.seal(r % sets)
+        # seal mode: the timed launches ARE the seal pass (and a profile's
+        # last --steps dispatches of the seal kernel stay the timed ones)
+        for r in range(0 if self.seal_only else reps):
+            pt = self.sets[r % sets][0]
+            assert self.seal(None, pt=pt, ct=ct_s) == 0
         e[1].record(self.stream)
         for r in range(reps):
-            self.open_((r - self.lag) % sets)
+            ct = self.sets[(r - self.lag) % sets][1]  # every set holds valid CT after the timed steps
+            assert A.dev_uniform(True, self.cipher, inp=ct.data_ptr(), out=back_s.data_ptr(),
+                                 in_stride=self.out_stride, out_stride=self.in_stride,
+                                 status=st_s.data_ptr(), flags=self.oflags, stream=self.sp,
+                                 **self._common()) == 0
         e[2].record(self.stream)
         torch.cuda.synchronize(self.dev)
-        return e[0].elapsed_time(e[1]) / reps, e[1].elapsed_time(e[2]) / reps
+        del ct_s, back_s, st_s
+        seal_ms = self.launch_ms if self.seal_only else e[0].elapsed_time(e[1]) / reps
+        return seal_ms, e[1].elapsed_time(e[2]) / reps
 
     def verify(self, config, rank, world):
         """After the timed region: every opened set's statuses are 0 and its
@@ -909,11 +957,11 @@ def n1_reference(args, cfg, A, torch, dev, rank, dist, wl, N, S, world):
             w1 = UniformWork(args, cfg, A, torch, dev, N * world, S * world,
                              shard(N * world, S * world, 0, 1))
             el = w1.timed(args.steps, args.warmup, None)
-            v = 2.0 * N * world * w1.L * args.steps / el / GIB
+            v = w1.dirs * N * world * w1.L * args.steps / el / GIB
             del w1
         else:
             el = wl.timed(args.steps, args.warmup, None)
-            v = 2.0 * N * wl.L * args.steps / el / GIB
+            v = wl.dirs * N * wl.L * args.steps / el / GIB
     v = max_over_ranks(dist, torch, dev, v)
     dist.barrier()
     return round(v, 2)
@@ -1075,7 +1123,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
                            bytes=int(lay["lens"][idx].sum()), states=len(states)))
     torch.cuda.synchronize(dev)
 
-    oflags = A.FLAG_VERIFY_FIRST if args.verify_first else 0
+    oflags = A.FLAG_ONE_PASS if args.one_pass else 0  # verify-first unless --one-pass
 
     def launch(g, open_, stream=sp, inp=None, out=None):
         inp = inp if inp is not None else (ct if open_ else pt)
@@ -1217,7 +1265,7 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
         mask = torch.cumsum(cov, 0, dtype=torch.int32)[:-1] > 0
         rt_ok = bool(torch.equal(back[mask], pt[mask]))
         del mask, cov
-        want = shard_golden("c5", rank, world, False)
+        want = shard_golden(args.config, rank, world, False)
         digest = "no golden for this rank"
         if want is not None:
             h = hashlib.sha256()
@@ -1240,20 +1288,20 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
         kname = f"chachapoly_seg_ragged<{'true' if open_ else 'false'}>"
     elif g["cipher"] == CHACHA:  # run_ragged: 8 lanes below 128 Ki records, else 4
         k = args.lanes or (8 if g["n"] < 131072 else 4)
-        kname = (f"chachapoly_open_ragged<{k}, true, {'true' if args.verify_first else 'false'}>"
+        kname = (f"chachapoly_open_ragged<{k}, true, {'false' if args.one_pass else 'true'}>"
                  if open_ else f"chachapoly_seal_ragged<{k}, true>")
     else:  # gcm_ragged_shape: (threads, records per group, lanes per record) by batch size
         n_aes = g["n"]
         wg, r, kl = (1024, 2, 4) if n_aes >= 131072 else ((1024, 2, 8) if n_aes >= 65536 else (256, 1, 4))
         kname = f"gcm_ragged_staged<{'true' if open_ else 'false'}, true, {wg}, false, {r}, {kl}>"
-    pmc = load_pmc("c5", kname)
+    pmc = load_pmc(args.config, kname)
     result = {
         "metric": "GiB/s device-resident AEAD encrypt+decrypt, mixed 64B-16KiB records per GPU",
         "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": "synthetic (SplitMix64 lengths, plaintext and keys, SURVEY.md 8d C5), resident in HBM",
-        "config": {"workload": cfg["workload"], "config": "c5", "records_per_gpu": R,
+        "config": {"workload": cfg["workload"], "config": args.config, "records_per_gpu": R,
                    "states_per_gpu": S, "payload_bytes_per_step": int(2 * payload * world),
                    "streams": 2 if side is not None else 1,
                    "join": args.c5_join if side is not None else None,
@@ -1268,8 +1316,8 @@ def run_mixed(args, cfg, A, torch, dev, rank, world, dist):
         "kernels_ms": {(("chacha" if gg["cipher"] == CHACHA else "aes") + ("_open" if o else "_seal")): round(m, 4)
                        for m, gg, o in per},
         "all_tags_verified": ok,
-        "open_order": ("verify-first" if args.verify_first else
-                       "ChaChaPoly one pass, AES-GCM verify-first (every AES-GCM open)"),
+        "open_order": ("ChaChaPoly one pass (NOISE_AEAD_FLAG_ONE_PASS), AES-GCM verify-first"
+                       if args.one_pass else "verify-first (the default, both ciphers)"),
     }
     if verify is not None:
         result["verified"] = verify.pop("ok")

@@ -198,14 +198,16 @@ int noise_aead_dev_prepare(int cipher_id, const uint8_t *d_raw_keys, uint32_t n_
  *           record's output is not written at all (in place: CT || tag read
  *           back as given; out of place: the output bytes keep whatever
  *           they held).  It costs nothing there.
- *         - CHACHAPOLY opens by default decrypt as they authenticate (one
- *           pass over the ciphertext), and a rejected record reads back in
- *           place exactly as given, out of place as ZEROED output bytes;
- *           until the kernel ends its output bytes may transiently hold
- *           unauthenticated plaintext, which the kernel undoes (restores /
- *           zeroes) before it completes.  With NOISE_AEAD_FLAG_VERIFY_FIRST
- *           they take the reference's order (cipher-chachapoly.c:135-141),
- *           as AESGCM does, at about 12 % of the batch rate.
+ *         - CHACHAPOLY opens take the same order by default (round 6; the
+ *           reference's cipher-chachapoly.c:135-141): authenticate, then
+ *           decrypt and write only verified records.  With the opt-in
+ *           NOISE_AEAD_FLAG_ONE_PASS a FAST-layout ChaChaPoly open decrypts
+ *           as it authenticates (one pass over the ciphertext, DESIGN.md
+ *           4.1b gives the rate difference), and a rejected record reads
+ *           back in place exactly as given, out of place as ZEROED output
+ *           bytes; until the kernel ends its output bytes may transiently
+ *           hold unauthenticated plaintext, which the kernel undoes
+ *           (restores / zeroes) before it completes.
  * Memory: input and output records must be either exactly in place
  * (in == out and in_stride == out_stride) or disjoint record by record:
  * with one stride for both sides the records may interleave (input and
@@ -229,7 +231,7 @@ typedef struct NoiseAeadUniform {
     uint32_t len;            /* <= 65535 - 16 */
     uint32_t ad_len;
     uint32_t lanes_per_record;
-    uint32_t flags;          /* NOISE_AEAD_FLAG_CT_GHASH, _VERIFY_FIRST (FAST is derived) */
+    uint32_t flags;          /* NOISE_AEAD_FLAG_CT_GHASH, _VERIFY_FIRST, _ONE_PASS (FAST is derived) */
 } NoiseAeadUniform;
 
 int noise_aead_dev_seal_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream);
@@ -246,8 +248,9 @@ int noise_aead_dev_open_uniform(int cipher_id, const NoiseAeadUniform *job, void
  * two jobs cannot share a kernel (unaligned layouts, different lane counts,
  * AESGCM without one state per 256 records, a VERIFY_FIRST ChaChaPoly open
  * on 4 or 8 lanes per record) the library issues the two launches on
- * `stream` instead; a VERIFY_FIRST open on one lane per record (the default
- * from 65 536 records) or on the staged AES-GCM kernel keeps the one launch. */
+ * `stream` instead; a verify-first open (the default) on one lane per record
+ * (the default from 65 536 records) or on the staged AES-GCM kernel keeps the
+ * one launch. */
 int noise_aead_dev_duplex_uniform(int cipher_id, const NoiseAeadUniform *seal_job,
                                   const NoiseAeadUniform *open_job, void *stream);
 
@@ -280,9 +283,9 @@ typedef struct NoiseAeadRagged {
  * processed: nothing is written and, when status is given, status[i] = 2 —
  * for seal too (status is optional there: 0 sealed, 2 refused).
  *
- * Open: a rejected record's output is handled as for the uniform open
- * (restored in place / zeroed out of place, or not written at all under
- * NOISE_AEAD_FLAG_VERIFY_FIRST).  Each record's input and output ranges must
+ * Open: a rejected record's output is handled as for the uniform open (not
+ * written at all by default; restored in place / zeroed out of place under
+ * NOISE_AEAD_FLAG_ONE_PASS).  Each record's input and output ranges must
  * be identical (in + in_off == out + out_off) or disjoint from every other
  * record's ranges; the descriptors live in device memory, so this is the
  * caller's guarantee (not checked).
@@ -306,14 +309,18 @@ typedef struct NoiseAeadRagged {
 
 /* Open only: authenticate first, decrypt only a verified record, and write
  * nothing for a rejected one (the reference's verify-then-decrypt order,
- * cipher-chachapoly.c:135-141, cipher-aesgcm.c:172-188).  Without it the
- * FAST-layout ChaChaPoly opens decrypt in one pass and undo a rejected
- * record's plaintext before the kernel ends (see the uniform open above);
- * AESGCM opens take this order whether or not it is set.  The host
- * paths (CipherState API, batch, wire) never expose unverified plaintext
- * either way: they stage records in library memory and copy out only
- * verified ones; they set this flag (strict order) by default. */
+ * cipher-chachapoly.c:135-141, cipher-aesgcm.c:172-188).  Since round 6
+ * this is the order of every open whether or not the flag is set; the flag
+ * stays accepted, and it overrides NOISE_AEAD_FLAG_ONE_PASS. */
 #define NOISE_AEAD_FLAG_VERIFY_FIRST 4u
+
+/* Open only, ChaChaPoly FAST layouts, opt-in: decrypt while authenticating
+ * (one pass over the ciphertext) and undo a rejected record's plaintext
+ * before the kernel ends — restored in place, zeroed out of place (see the
+ * uniform open above).  Faster on the device API; the
+ * host paths (CipherState API, batch, wire) never set it.  AESGCM opens and
+ * non-FAST layouts ignore it (they always verify first). */
+#define NOISE_AEAD_FLAG_ONE_PASS 8u
 
 int noise_aead_dev_seal_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);
 int noise_aead_dev_open_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream);

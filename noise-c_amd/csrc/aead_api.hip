@@ -67,8 +67,8 @@ bool uniform_fast(const NoiseAeadUniform *j, bool open)
    back-to-back seal and open launches 1624-1636 vs 1410-1415 GiB/s at four
    lanes, while a 64 Ki-record job alone (one wave per SIMD) runs 3 % faster
    at four lanes (1315-1321 vs 1280-1283, profiles/r04/separate_lanes_ab.jsonl)
-   — except a VERIFY_FIRST open, which the 4/8-lane staged kernels do not
-   run.  NOISE_AEAD_SOLO=0 keeps the 4-lane kernels everywhere (A/B runs). */
+   — except a verify-first open (the default), which the 4/8-lane staged
+   kernels do not run.  NOISE_AEAD_SOLO=0 keeps the 4-lane kernels everywhere (A/B runs). */
 constexpr uint32_t SOLO_MIN_RECORDS = 65536;
 constexpr uint32_t SOLO_MIN_STANDALONE = 2 * SOLO_MIN_RECORDS;
 
@@ -110,6 +110,8 @@ int standalone_lanes(uint32_t n)
     return seg_mode() == 2 ? 2 : 0;
 }
 
+bool flags_vf(uint32_t flags);
+
 int uniform_lanes(const NoiseAeadUniform *j, bool open, bool duplex)
 {
     if (j->lanes_per_record) return (int)j->lanes_per_record;
@@ -117,7 +119,7 @@ int uniform_lanes(const NoiseAeadUniform *j, bool open, bool duplex)
         if (duplex) return 1;
         const int k = standalone_lanes(j->n_records);
         if (k) return k;
-        if (open && (j->flags & NOISE_AEAD_FLAG_VERIFY_FIRST)) return 1;
+        if (open && flags_vf(j->flags)) return 1;
     }
     return auto_lanes(j->n_records, 0);
 }
@@ -127,6 +129,10 @@ int uniform_lanes(const NoiseAeadUniform *j, bool open, bool duplex)
    record length, chachapoly_seg.hip); smaller ones keep the windowed 4/8-lane
    kernels and the wide groups of the latency path. */
 constexpr uint32_t SEG_RAGGED_MIN = 16384;
+/* The plan packs record << 6 | segment into 32 bits (chachapoly_seg.hip
+   seg_plan_place) and counts lanes in 32 bits: batches of 2^26 records or
+   more keep the windowed kernels. */
+constexpr uint32_t SEG_RAGGED_MAX = 1u << 26;
 
 void job_span(const NoiseAeadUniform *j, bool out, bool open, uint64_t &lo, uint64_t &hi);
 
@@ -198,16 +204,22 @@ UniformArgs to_args(const NoiseAeadUniform *j)
     return a;
 }
 
-/* The open order of a job: verify first under NOISE_AEAD_FLAG_VERIFY_FIRST,
-   and always for AES-GCM — there it costs nothing (C3 732 vs 726 GiB/s, the
-   C5 AES-GCM open 0.77 vs 0.82 ms: the GHASH-only pass, then CTR for the
-   verified records, profiles/r04_round/), so AES-GCM opens have the
-   reference's order (cipher-aesgcm.c:172-188) on every path.  ChaChaPoly
-   keeps the one-pass order by default (verify-first costs about 12 %,
-   DESIGN.md 4.1b). */
+/* The open order of a job: verify first — the reference's order
+   (cipher-chachapoly.c:135-141, cipher-aesgcm.c:172-188) — for every open
+   unless a ChaChaPoly job opts into NOISE_AEAD_FLAG_ONE_PASS (round 6,
+   VERDICT r5 item 1; the one-pass order was the ChaChaPoly default through
+   round 5, DESIGN.md 4.1b gives the cost).  AES-GCM opens always verify
+   first: there it costs nothing (C3 732 vs 726 GiB/s, the C5 AES-GCM open
+   0.77 vs 0.82 ms: the GHASH-only pass, then CTR for the verified records,
+   profiles/r04_round/).  VERIFY_FIRST overrides ONE_PASS. */
+bool flags_vf(uint32_t flags)
+{
+    return (flags & NOISE_AEAD_FLAG_VERIFY_FIRST) || !(flags & NOISE_AEAD_FLAG_ONE_PASS);
+}
+
 bool open_vf(int cipher_id, uint32_t flags, bool open)
 {
-    return open && ((flags & NOISE_AEAD_FLAG_VERIFY_FIRST) || cipher_id == NOISE_CIPHER_AESGCM);
+    return open && (flags_vf(flags) || cipher_id == NOISE_CIPHER_AESGCM);
 }
 
 
@@ -372,7 +384,7 @@ int run_ragged(int cipher_id, const NoiseAeadRagged *job, void *stream, bool ope
            records vs 4 lanes, profiles/r02/c5_lanes_ab.jsonl) */
         if (!job->lanes_per_record && k == 4 && job->n_records < 2u * 65536u) k = 8;
         if (!job->lanes_per_record && (job->flags & NOISE_AEAD_FLAG_FAST) && job->n_records >= SEG_RAGGED_MIN &&
-            seg_enabled())
+            job->n_records < SEG_RAGGED_MAX && seg_enabled())
             return chacha_ragged_seg(a, open, s);
         return chacha_ragged(a, k, open, (job->flags & NOISE_AEAD_FLAG_FAST) != 0, s);
     }

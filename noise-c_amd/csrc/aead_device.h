@@ -150,6 +150,107 @@ NA_DEV void chacha20_2block_pre(const uint32_t key[8], const ChaPre &p, uint32_t
     y[12] += c1; y[14] += iv_lo; y[15] += iv_hi;
 }
 
+/* Two blocks of one key and nonce in lock step, issued in RUNS (round 6).
+   gfx950 issues the fast integer class (v_add_u32, v_xor_b32: ~2.1
+   SIMD-cycles per wave-instruction with >= 2 waves) and the slow class
+   (v_alignbit_b32 and every other shift/rotate: ~4.1) at their own rates
+   only when a SIMD's waves issue the classes apart: any mix within one
+   wave's stream ran at ~4 per instruction, whatever the run lengths
+   (profiles/r01_runs_mix.log).  tools/microbench/xwave.hip: with the
+   quarter-rounds of several blocks in lock step every ChaCha sub-step is a
+   run of fast ops (the adds, then the xors) followed by a run of rotates;
+   raising the wave's priority (s_setprio) for its rotate run and dropping it
+   for its fast run lets the SIMD's other waves' fast runs fill the issue
+   slots a rotate run leaves (profiles/r06/xwave.log).  The runs are fixed
+   by inline asm (hipcc's own schedule interleaves the classes).  PS / PF:
+   the priority of the rotate / fast runs (PS < 0: no s_setprio). */
+constexpr int NA_CQR[2][4][4] = {{{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15}},
+                                 {{0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}}};
+
+#define NA_RUN8(op, d0, d1, d2, d3, d4, d5, d6, d7, s0, s1, s2, s3, s4, s5, s6, s7)                      \
+    asm volatile(op " %0, %0, %8\n\t" op " %1, %1, %9\n\t" op " %2, %2, %10\n\t" op " %3, %3, %11\n\t" op \
+                    " %4, %4, %12\n\t" op " %5, %5, %13\n\t" op " %6, %6, %14\n\t" op " %7, %7, %15"    \
+                 : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3), "+v"(d4), "+v"(d5), "+v"(d6), "+v"(d7)        \
+                 : "v"(s0), "v"(s1), "v"(s2), "v"(s3), "v"(s4), "v"(s5), "v"(s6), "v"(s7))
+
+template <int P>
+NA_DEV void na_setprio()
+{
+    if constexpr (P >= 0) __builtin_amdgcn_s_setprio(P);
+}
+
+/* one sub-step of a half round over the 2 x 4 quarter-rounds: dst += src,
+   x ^= dst (the fast run), x <<<= N (the rotate run) */
+template <int RND, int DST, int SRC, int X, int N, int PS, int PF>
+NA_DEV void chacha_substep2(uint32_t (&x)[16], uint32_t (&y)[16])
+{
+#define NA_XW(z, q, k) z[NA_CQR[RND][q][k]]
+    na_setprio<PF>();
+    NA_RUN8("v_add_u32", NA_XW(x, 0, DST), NA_XW(x, 1, DST), NA_XW(x, 2, DST), NA_XW(x, 3, DST), NA_XW(y, 0, DST),
+            NA_XW(y, 1, DST), NA_XW(y, 2, DST), NA_XW(y, 3, DST), NA_XW(x, 0, SRC), NA_XW(x, 1, SRC),
+            NA_XW(x, 2, SRC), NA_XW(x, 3, SRC), NA_XW(y, 0, SRC), NA_XW(y, 1, SRC), NA_XW(y, 2, SRC),
+            NA_XW(y, 3, SRC));
+    NA_RUN8("v_xor_b32", NA_XW(x, 0, X), NA_XW(x, 1, X), NA_XW(x, 2, X), NA_XW(x, 3, X), NA_XW(y, 0, X),
+            NA_XW(y, 1, X), NA_XW(y, 2, X), NA_XW(y, 3, X), NA_XW(x, 0, DST), NA_XW(x, 1, DST), NA_XW(x, 2, DST),
+            NA_XW(x, 3, DST), NA_XW(y, 0, DST), NA_XW(y, 1, DST), NA_XW(y, 2, DST), NA_XW(y, 3, DST));
+    na_setprio<PS>();
+    asm volatile("v_alignbit_b32 %0, %0, %0, %8\n\tv_alignbit_b32 %1, %1, %1, %8\n\t"
+                 "v_alignbit_b32 %2, %2, %2, %8\n\tv_alignbit_b32 %3, %3, %3, %8\n\t"
+                 "v_alignbit_b32 %4, %4, %4, %8\n\tv_alignbit_b32 %5, %5, %5, %8\n\t"
+                 "v_alignbit_b32 %6, %6, %6, %8\n\tv_alignbit_b32 %7, %7, %7, %8"
+                 : "+v"(NA_XW(x, 0, X)), "+v"(NA_XW(x, 1, X)), "+v"(NA_XW(x, 2, X)), "+v"(NA_XW(x, 3, X)),
+                   "+v"(NA_XW(y, 0, X)), "+v"(NA_XW(y, 1, X)), "+v"(NA_XW(y, 2, X)), "+v"(NA_XW(y, 3, X))
+                 : "i"(32 - N));
+#undef NA_XW
+}
+
+template <int RND, int PS, int PF>
+NA_DEV void chacha_halfround2(uint32_t (&x)[16], uint32_t (&y)[16])
+{
+    chacha_substep2<RND, 0, 1, 3, 16, PS, PF>(x, y);
+    chacha_substep2<RND, 2, 3, 1, 12, PS, PF>(x, y);
+    chacha_substep2<RND, 0, 1, 3, 8, PS, PF>(x, y);
+    chacha_substep2<RND, 2, 3, 1, 7, PS, PF>(x, y);
+}
+
+/* chacha20_2block_pre's result (blocks c0, c1 of one key and nonce), the
+   rounds issued in runs; PEND: the priority left set on return (< 0: as the
+   last rotate run left it) */
+template <int PS, int PF, int PEND>
+NA_DEV void chacha20_2block_runs(const uint32_t key[8], const ChaPre &p, uint32_t c0, uint32_t c1,
+                                 uint32_t iv_lo, uint32_t iv_hi, uint32_t (&x)[16], uint32_t (&y)[16])
+{
+#define NA_COL0(z, ctr)                                                   \
+    {                                                                     \
+        uint32_t a = p.a0, b = key[0], c = key[4], d = (ctr);             \
+        d ^= a; d = rotl(d, 16);                                          \
+        c += d; b ^= c; b = rotl(b, 12);                                  \
+        a += b; d ^= a; d = rotl(d, 8);                                   \
+        c += d; b ^= c; b = rotl(b, 7);                                   \
+        z[0] = a; z[4] = b; z[8] = c; z[12] = d;                          \
+        z[1] = p.c1[0]; z[5] = p.c1[1]; z[9] = p.c1[2]; z[13] = p.c1[3];  \
+        z[2] = p.c2[0]; z[6] = p.c2[1]; z[10] = p.c2[2]; z[14] = p.c2[3]; \
+        z[3] = p.c3[0]; z[7] = p.c3[1]; z[11] = p.c3[2]; z[15] = p.c3[3]; \
+    }
+    NA_COL0(x, c0)
+    NA_COL0(y, c1)
+#undef NA_COL0
+    chacha_halfround2<1, PS, PF>(x, y); /* round 1's diagonal half */
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        chacha_halfround2<0, PS, PF>(x, y);
+        chacha_halfround2<1, PS, PF>(x, y);
+    }
+    na_setprio<PEND>();
+    const uint32_t k0[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { x[i] += k0[i]; y[i] += k0[i]; }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { x[4 + i] += key[i]; y[4 + i] += key[i]; }
+    x[12] += c0; x[14] += iv_lo; x[15] += iv_hi;
+    y[12] += c1; y[14] += iv_lo; y[15] += iv_hi;
+}
+
 /* ------------------------------------------------------------- Poly1305 */
 
 constexpr uint32_t M26 = 0x3ffffffu;
@@ -552,13 +653,11 @@ NA_DEV void mask_unit(uint32_t w[16], uint32_t n)
    branches. */
 NA_DEV void prio_by_progress(uint32_t done, uint32_t total)
 {
-#ifndef NA_NO_PRIO_BALANCE
     const uint32_t q = (4 * done) / (total ? total : 1);
     if (q == 0) __builtin_amdgcn_s_setprio(3);
     else if (q == 1) __builtin_amdgcn_s_setprio(2);
     else if (q == 2) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 } // namespace na

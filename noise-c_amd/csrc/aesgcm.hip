@@ -23,9 +23,6 @@
  */
 #include "aead_device.h"
 #include "aead_kernels.h"
-#ifdef NA_AB_KERNELS
-#include "aes_bs.h" /* the bitsliced A/B kernels only */
-#endif
 
 namespace na {
 
@@ -921,11 +918,7 @@ __global__ __launch_bounds__(GCM_WG) void gcm_duplex_staged(UniformArgs s, Unifo
    a scalar load's wait is lgkmcnt(0), which also drains the LDS lookups in
    flight: measured (profiles/r05/rk_scalar_ab.txt) the ragged seal gains
    3.5 % (0.787 -> 0.760 ms at C5), the verify-first ragged open loses 14 %
-   and C3's fused duplex 1.5 %, so only the ragged seal takes it.
-   NA_RK_SCALAR=0: the LDS copy everywhere (A/B). */
-#ifndef NA_RK_SCALAR
-#define NA_RK_SCALAR 1
-#endif
+   and C3's fused duplex 1.5 %, so only the ragged seal takes it. */
 typedef const __attribute__((address_space(4))) uint32_t *RkS;
 
 /* the wave-uniform address p as a constant-address-space pointer */
@@ -971,294 +964,6 @@ __global__ __launch_bounds__(GCM_WG) void gcm_duplex_fused(UniformArgs s, Unifor
     if (b < o_blocks) gcm_staged_rec<true, CT>(o, TE, L.h4[1], L.rk[1], b);
 }
 
-#ifdef NA_AB_KERNELS
-/* Built only into the A/B variant (`make -C noise-c_amd variant NAME=ab
-   DEFS=-DNA_AB_KERNELS`): the round-4 bitsliced-AES kernels, measured and
-   rejected, kept so that record can be re-run; the product
-   library does not contain them. */
-/* ---------------------- bitsliced (uniform FAST, one state per workgroup)
- *
- * Round 4 (decide AES-GCM's structure in the full kernel).  A
- * lane pair owns one record.  The record's counter blocks ctr = 0 .. run in
- * groups of 32 (ctr 32g .. 32g+31): the pair computes a group's key stream
- * with the bitsliced AES of aes_bs.h (no tables, constant-time), XORs it
- * into the record's data (lane L: bytes 8L..8L+7 of every block) and feeds
- * GHASH from registers.  GHASH position p of the GCM input (AD empty:
- * p = 1..M the CT blocks, p = M + 1 = n the length block) is ctr p + 1, so
- * group g holds positions 32g - 1 .. 32g + 30; lane L runs Horner with H
- * over the 16 positions 32g + 16L - 1 .. (one DPP exchange makes its blocks
- * whole), jumping over the partner's 16 with H^16 = (H^8)^2 between groups.
- * With e_L its last position, GHASH = y_0 H^(n - e_0) + y_1 H^(n - e_1)
- * (one of the exponents is 0).  ctr 1 = J0 gives the tag mask.  Tables in
- * LDS: the round-key masks, multiply-by-H and multiply-by-H^8.
- */
-/* NT threads per workgroup; T8: multiply-by-H as an 8-bit positional table
-   (16 lookups per block instead of 32; 64 KiB, so one 1024-thread
-   workgroup per CU shares it) */
-template <int NT, bool T8>
-struct GcmBsLds {
-    uint32_t km[15 * 128]; /* bs_mask_entry layout */
-    uint4 h1[T8 ? 16 * 256 : GHASH_TAB_ENTRIES];
-    uint4 h8[GHASH_TAB_ENTRIES];
-    /* each thread's GCM state parked across a group's AES (the AES needs all
-       but ~10 of the 128 VGPRs): y[4], E(J0) words, last position, nonce */
-    uint32_t park[9][NT];
-};
-constexpr uint32_t GCM_BS_RECS = 128;   /* records per 256-thread workgroup */
-constexpr uint32_t GCM_BS8_RECS = 512;  /* records per 1024-thread workgroup (8-bit H table) */
-
-template <int NT, bool T8>
-NA_DEV void gcm_bs_fill(GcmBsLds<NT, T8> &S, const AesCtx *ctx)
-{
-    for (uint32_t e = threadIdx.x; e < 15 * 128; e += NT) S.km[e] = bs_mask_entry(ctx->rk, e);
-    const uint4 *t1 = (const uint4 *)ctx->tab[0], *t8 = (const uint4 *)ctx->tab8;
-    for (uint32_t i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += NT) S.h8[i] = t8[i];
-    if constexpr (T8) { /* byte position p, value v: the two nibble entries' sum */
-        for (uint32_t e = threadIdx.x; e < 16 * 256; e += NT) {
-            const uint32_t p = e >> 8, v = e & 255;
-            const uint4 hi = t1[(2 * p) * 16 + (v >> 4)], lo = t1[(2 * p + 1) * 16 + (v & 15)];
-            S.h1[e] = make_uint4(hi.x ^ lo.x, hi.y ^ lo.y, hi.z ^ lo.z, hi.w ^ lo.w);
-        }
-    } else {
-        for (uint32_t i = threadIdx.x; i < GHASH_TAB_ENTRIES; i += NT) S.h1[i] = t1[i];
-    }
-}
-
-/* y <- y * Y with Y's 8-bit positional table (byte p of the LE words) */
-NA_DEV void gh_mul_lds8(uint32_t y[4], const uint4 *tab)
-{
-    uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-#pragma unroll
-    for (int p = 0; p < 16; p += 2) {
-        const uint32_t b0 = (y[p >> 2] >> (8 * (p & 3))) & 255u;
-        const uint32_t b1 = (y[(p + 1) >> 2] >> (8 * ((p + 1) & 3))) & 255u;
-        const uint4 e = tab[p * 256 + b0];
-        const uint4 f = tab[(p + 1) * 256 + b1];
-        r0 = xor3(r0, e.x, f.x); r1 = xor3(r1, e.y, f.y);
-        r2 = xor3(r2, e.z, f.z); r3 = xor3(r3, e.w, f.w);
-    }
-    y[0] = r0; y[1] = r1; y[2] = r2; y[3] = r3;
-}
-
-/* y <- y * H^k, 0 <= k <= 16 (the context's H^1..H^4 and H^8 tables) */
-NA_DEV void gh_mul_hpow(uint32_t y[4], const AesCtx *ctx, uint32_t k)
-{
-    while (k >= 8) {
-        gh_mul(y, (const uint4 *)ctx->tab8);
-        k -= 8;
-    }
-    if (k >= 4) {
-        gh_mul(y, (const uint4 *)ctx->tab[3]);
-        k -= 4;
-    }
-    if (k) gh_mul(y, (const uint4 *)ctx->tab[k - 1]);
-}
-
-/* 8 bytes at p (8-B aligned), the first nb (0..8) of them */
-NA_DEV void st8(uint8_t *p, uint32_t nb, uint32_t w0, uint32_t w1)
-{
-    if (nb >= 8) {
-        *(uint2 *)p = make_uint2(w0, w1);
-    } else if (nb) {
-        const uint32_t w[4] = {w0, w1, 0u, 0u};
-        store16(p, nb, w);
-    }
-}
-
-/* One record per lane pair.  Returns (open) whether the tag verified; the
-   plaintext is written as it is produced (one pass) and repaired by the
-   caller on a MAC failure. */
-template <bool OPEN, int NT, bool T8>
-NA_DEV bool gcm_bs_rec(const UniformArgs &a, GcmBsLds<NT, T8> &S, const AesCtx *ctx, uint32_t rec0, uint64_t nonce)
-{
-    const uint32_t L = threadIdx.x & 1, tid = threadIdx.x;
-    const uint32_t len = a.len, M = (len + 15) / 16, n = M + 1;
-    const uint32_t NG = (n + 2 + 31) / 32;
-    uint32_t (*park)[NT] = S.park;
-    park[0][tid] = 0; park[1][tid] = 0; park[2][tid] = 0; park[3][tid] = 0;
-    park[6][tid] = 0xFFFFFFFFu; /* e: no GHASH position yet */
-    park[7][tid] = (uint32_t)nonce; park[8][tid] = (uint32_t)(nonce >> 32);
-    for (uint32_t g = 0; g < NG; ++g) {
-        uint32_t x[2][32];
-        bs2_ctr_group(S.km, L, park[8][tid], park[7][tid], g, x);
-        if (g == 0) { park[4][tid] = x[0][1]; park[5][tid] = x[1][1]; } /* E(J0) */
-        const uint32_t rec_raw = rec0 + tid / 2;
-        const bool live = rec_raw < a.n_records;
-        const uint32_t rc = live ? rec_raw : a.n_records - 1;
-        const uint8_t *src = a.in + (size_t)rc * a.in_stride;
-        uint8_t *dst = a.out + (size_t)rc * a.out_stride;
-        /* data blocks d = 32g + i - 2: this lane's 8 bytes in, key stream
-           XOR, out; x becomes the CT (the GHASH input), masked to len */
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            const int d = (int)(32 * g) + i - 2;
-            if (d < 0 || d >= (int)M) {
-                x[0][i] = x[1][i] = 0;
-                continue;
-            }
-            const uint32_t nb = min(len - 16u * (uint32_t)d, 16u);
-            const uint32_t nbl = nb > 8 * L ? min(nb - 8 * L, 8u) : 0u;
-            const uint2 v = *(const uint2 *)(src + 16 * d + 8 * L); /* FAST: readable */
-            const uint32_t o0 = v.x ^ x[0][i], o1 = v.y ^ x[1][i];
-            if (live) st8(dst + 16 * d + 8 * L, nbl, o0, o1);
-            const uint32_t m0 = nbl >= 4 ? 0xffffffffu : (nbl ? (1u << (8 * nbl)) - 1u : 0u);
-            const uint32_t m1 = nbl >= 8 ? 0xffffffffu : (nbl > 4 ? (1u << (8 * (nbl - 4))) - 1u : 0u);
-            x[0][i] = (OPEN ? v.x : o0) & m0;
-            x[1][i] = (OPEN ? v.y : o1) & m1;
-            if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0); /* a few blocks' loads in flight, not 32 */
-        }
-        /* the length block, position n = slot n + 1 - 32g: BE64(8|AD|) ||
-           BE64(8|CT|), AD empty (lane 1 holds words 2, 3) */
-        if (n + 1 >= 32 * g && n + 1 < 32 * g + 32) {
-            const uint32_t i = n + 1 - 32 * g;
-            const uint64_t cb = (uint64_t)len * 8;
-#pragma unroll
-            for (int q = 0; q < 32; ++q)
-                if ((uint32_t)q == i && L) {
-                    x[0][q] = __builtin_bswap32((uint32_t)(cb >> 32));
-                    x[1][q] = __builtin_bswap32((uint32_t)cb);
-                }
-        }
-        /* whole blocks for the lane's 16 slots 16L + t: lane 0 takes words
-           2, 3 of slots 0..15 from lane 1, lane 1 words 0, 1 of 16..31 */
-        const int first = (int)(32 * g) + 16 * (int)L - 1; /* position of slot 16L */
-        /* pair-uniform (the DPP exchange reads the partner lane, which must
-           be active); the lane's own Horner only where it holds positions */
-        if ((int)(32 * g) - 1 <= (int)n) {
-            const bool mine = first <= (int)n;
-            uint32_t y[4] = {park[0][tid], park[1][tid], park[2][tid], park[3][tid]};
-            if (mine && (int)park[6][tid] >= 0) { /* jump over the partner's 16 positions: H^16 */
-                gh_mul_lds(y, S.h8);
-                gh_mul_lds(y, S.h8);
-            }
-#pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const uint32_t s0 = L ? x[0][t] : x[0][16 + t], s1 = L ? x[1][t] : x[1][16 + t];
-                const uint32_t r0 = bs_partner(s0), r1 = bs_partner(s1);
-                const int p = first + t;
-                if (mine && p >= 1 && p <= (int)n) {
-                    y[0] ^= L ? r0 : x[0][t];
-                    y[1] ^= L ? r1 : x[1][t];
-                    y[2] ^= L ? x[0][16 + t] : r0;
-                    y[3] ^= L ? x[1][16 + t] : r1;
-                    if constexpr (T8) gh_mul_lds8(y, S.h1);
-                    else gh_mul_lds(y, S.h1);
-                }
-            }
-            if (mine) {
-                park[0][tid] = y[0]; park[1][tid] = y[1]; park[2][tid] = y[2]; park[3][tid] = y[3];
-                park[6][tid] = (uint32_t)min((int)n, first + 15);
-            }
-        }
-    }
-    /* GHASH = y_0 H^(n - e_0) + y_1 H^(n - e_1) */
-    uint32_t y[4] = {park[0][tid], park[1][tid], park[2][tid], park[3][tid]};
-    gh_mul_hpow(y, ctx, (uint32_t)((int)n - (int)park[6][tid]));
-    uint32_t G[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) G[w] = y[w] ^ bs_partner(y[w]);
-    const uint32_t t0 = G[2 * L] ^ park[4][tid], t1 = G[2 * L + 1] ^ park[5][tid];
-    const uint32_t rec_raw = rec0 + tid / 2;
-    const bool live = rec_raw < a.n_records;
-    const uint32_t rc = live ? rec_raw : a.n_records - 1;
-    if (!OPEN) {
-        if (live) *(uint2 *)(a.out + (size_t)rc * a.out_stride + len + 8 * L) = make_uint2(t0, t1);
-        return true;
-    }
-    const uint2 got = *(const uint2 *)(a.in + (size_t)rc * a.in_stride + len + 8 * L);
-    const uint32_t bad = (got.x ^ t0) | (got.y ^ t1);
-    return (bad | bs_partner(bad)) == 0;
-}
-
-/* In-place repair of a rejected record (MAC failure, one-pass open): its
-   plaintext XORed with the key stream once more is the ciphertext as given
-   (cipher-aesgcm.c:184-186 leaves a rejected buffer untouched). */
-template <int NT, bool T8>
-NA_DEV void gcm_bs_repair(const UniformArgs &a, const GcmBsLds<NT, T8> &S, uint32_t rc, bool bad, uint64_t nonce)
-{
-    const uint32_t L = threadIdx.x & 1;
-    uint8_t *dst = a.out + (size_t)rc * a.out_stride;
-    const uint32_t len = a.len, M = (len + 15) / 16, n = M + 1, NG = (n + 2 + 31) / 32;
-    for (uint32_t g = 0; g < NG; ++g) {
-        uint32_t x[2][32];
-        bs2_ctr_group(S.km, L, (uint32_t)(nonce >> 32), (uint32_t)nonce, g, x);
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            const int d = (int)(32 * g) + i - 2;
-            if (d < 0 || d >= (int)M || !bad) continue;
-            const uint32_t nb = min(len - 16u * (uint32_t)d, 16u);
-            const uint32_t nbl = nb > 8 * L ? min(nb - 8 * L, 8u) : 0u;
-            const uint2 v = *(const uint2 *)(dst + 16 * d + 8 * L);
-            st8(dst + 16 * d + 8 * L, nbl, v.x ^ x[0][i], v.y ^ x[1][i]);
-        }
-    }
-}
-
-template <bool OPEN, int NT, bool T8>
-NA_DEV void gcm_bs_wg(const UniformArgs &a, GcmBsLds<NT, T8> &S, uint32_t blk)
-{
-    const uint32_t rec0 = blk * (NT / 2);
-    const uint32_t st = rec0 / a.rps; /* one state per workgroup (host-checked) */
-    const AesCtx *ctx = (const AesCtx *)a.keys + st;
-    gcm_bs_fill(S, ctx);
-    __syncthreads();
-    const uint32_t rec_raw = rec0 + threadIdx.x / 2;
-    const bool live = rec_raw < a.n_records;
-    const uint32_t rc = live ? rec_raw : a.n_records - 1;
-    const uint64_t nonce = a.nonce_base[st] + (uint64_t)(rc - st * a.rps);
-    const bool ok = gcm_bs_rec<OPEN>(a, S, ctx, rec0, nonce);
-    if (!OPEN) return;
-    if (live && (threadIdx.x & 1) == 0 && a.status) a.status[rec_raw] = ok ? 0 : 1;
-    const bool bad = live && !ok;
-    if (__ballot(bad) == 0) return;
-    if (a.in == a.out && a.in_stride == a.out_stride) {
-        __threadfence(); /* this wave's plaintext stores, visible to its reads */
-        gcm_bs_repair(a, S, rc, bad, nonce);
-    } else if (bad) {
-        scrub_rejected(a.out + (size_t)rc * a.out_stride, a.in + (size_t)rc * a.in_stride, a.len,
-                       threadIdx.x & 1, 2);
-    }
-}
-
-#define NA_BS_OCC __attribute__((amdgpu_waves_per_eu(4)))
-
-template <bool OPEN>
-__global__ __launch_bounds__(256) NA_BS_OCC void gcm_bs_uniform(UniformArgs a)
-{
-    __shared__ GcmBsLds<256, false> S;
-    gcm_bs_wg<OPEN>(a, S, blockIdx.x);
-}
-
-template <bool OPEN>
-__global__ __launch_bounds__(1024) NA_BS_OCC void gcm_bs8_uniform(UniformArgs a)
-{
-    __shared__ GcmBsLds<1024, true> S;
-    gcm_bs_wg<OPEN>(a, S, blockIdx.x);
-}
-
-#ifndef NA_NO_SETUP_KERNELS /* one definition: launch_aes.hip's (worker.hip includes this file too) */
-/* seal job s and open job o in one launch, workgroups alternating */
-template <int NT, bool T8>
-__global__ __launch_bounds__(NT) NA_BS_OCC void gcm_bs_duplex(UniformArgs s, UniformArgs o, uint32_t s_blocks,
-                                                              uint32_t o_blocks)
-{
-    __shared__ GcmBsLds<NT, T8> S;
-    const uint32_t n = min(s_blocks, o_blocks);
-    uint32_t b = blockIdx.x;
-    bool open;
-    if (b < 2 * n) {
-        open = b & 1;
-        b >>= 1;
-    } else {
-        open = o_blocks > s_blocks;
-        b -= n;
-    }
-    if (open) gcm_bs_wg<true>(o, S, b);
-    else gcm_bs_wg<false>(s, S, b);
-}
-#endif
-
-#endif /* NA_AB_KERNELS */
 
 /* ------------------------------ staged ragged (any mix of states / lengths)
  *
@@ -1470,7 +1175,6 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
         const int sl = d.ctx_off == slot_off[0] ? 0 : (d.ctx_off == slot_off[1] ? 1 : -1);
         const bool vf = OPEN && a.vf;
         bool done = false;
-#if NA_RK_SCALAR
         if constexpr (!OPEN) { /* seals only: measured slower in the opens and in C3's fused duplex */
             const int s0 = __builtin_amdgcn_readfirstlane(sl);
             if (s0 >= 0 && __all(sl == s0)) { /* the wave's records share an LDS slot */
@@ -1479,7 +1183,6 @@ __global__ __launch_bounds__(WG) void gcm_ragged_staged(RaggedArgs a)
                 done = true;
             }
         }
-#endif
         if (done) {
         } else if (sl >= 0)
             ok = gcm_record_staged<OPEN, FAST, CT, KL>(rv, l, TE, tpl, L.rk[sl], L.h4[sl], vf);

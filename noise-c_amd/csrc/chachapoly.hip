@@ -34,13 +34,14 @@
  * in the loop; only the record's last unit and the tag take an exact-size
  * path, after the loop.  The generic path accepts any alignment.
  *
- * Decrypt comes in two forms.  The two-pass opens (open_il, open_ct)
- * verify first, then decrypt; a record whose tag fails writes nothing
+ * Decrypt comes in two forms.  The verify-first opens (open_il, open_ct,
+ * the one-lane AUTH + DEC passes: the default since round 6) verify first,
+ * then decrypt; a record whose tag fails writes nothing
  * (cipher-chachapoly.c:139-141) and the second ciphertext read is served by
- * L2.  The one-pass opens (open_il_1p, open_il_staged: the default of the
- * FAST layouts) decrypt as they authenticate and undo the plaintext of a
- * rejected record before the kernel ends (restored in place, zeroed out of
- * place); NOISE_AEAD_FLAG_VERIFY_FIRST selects the two-pass form.
+ * L2 / MALL.  The one-pass opens (open_il_1p, open_il_staged, solo_pass
+ * OPEN1: the opt-in NOISE_AEAD_FLAG_ONE_PASS of the FAST layouts) decrypt as
+ * they authenticate and undo the plaintext of a rejected record before the
+ * kernel ends (restored in place, zeroed out of place).
  */
 #include "aead_device.h"
 #include "aead_kernels.h"
@@ -376,18 +377,15 @@ NA_DEV void poly_tree_close(Fe acc, int k, const Fe &r, const Mul &mr, uint32_t 
    computing a block no one reads.  The issue slots are the same; what it
    saves is energy, and the chip holds its clock by energy under this load
    (MI355X_MICROARCH.md, DVFS give-back): C4 +1.1 %, perf +0.9 % in three
-   interleaved rounds (profiles/r02/mask_idle_ab.jsonl).  -DNA_NO_MASK_IDLE
-   restores the unmasked step for A/B runs. */
+   interleaved rounds (profiles/r02/mask_idle_ab.jsonl). */
 NA_DEV void slot_block(const uint32_t key[8], const ChaPre &pre, int v, uint32_t n_lo,
                        uint32_t n_hi, uint32_t x[16])
 {
-#ifndef NA_NO_MASK_IDLE
     if (v < 0) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = 0;
         return;
     }
-#endif
     chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
 }
 
@@ -542,28 +540,8 @@ NA_DEV bool open_il_1p(const RecView &rv, int k)
     return false;
 }
 
-/* Open's authentication pass has only Poly1305 (≈200 instructions per unit)
-   to hide each unit's load behind, so with one unit prefetched in registers
-   it waits on memory.  The FAST ragged kernels stream it through a ring of
-   three 4 KB LDS tiles per wave instead (LDS-DMA, two units in flight, no
-   VGPRs): three distinct arrays, so each unrolled step's tile is static and
-   the reads wait only for their own tile's DMA. */
-struct AuthRing { uint4 *t0, *t1, *t2; };
-
-template <int K>
-NA_DEV void auth_dma(const RecView &rv, const GroupCtx<K> &g, int k, uint32_t m, uint4 *t)
-{
-    const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
-    const bool ok = m < g.steps && v >= 1; /* else unit 0: FAST slots are readable */
-    const uint8_t *p = rv.src + 64u * (ok ? (uint32_t)v - 1 : 0u);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-        __builtin_amdgcn_global_load_lds((const void *)(p + 16 * c), (lds_void *)(t + 64 * c),
-                                         16, 0, 0);
-}
-
-template <int K, bool FAST, bool RING = false>
-NA_DEV bool open_il(const RecView &rv, int k, AuthRing ring = AuthRing{})
+template <int K, bool FAST>
+NA_DEV bool open_il(const RecView &rv, int k)
 {
     uint32_t key[8];
     load_key(rv.key, key);
@@ -592,52 +570,6 @@ NA_DEV bool open_il(const RecView &rv, int k, AuthRing ring = AuthRing{})
     /* phase 1: authenticate the ciphertext */
     uint32_t wn[16], wc[16];
     bool seen = false;
-    if constexpr (RING) {
-        static_assert(FAST, "the LDS ring reads whole units");
-        const uint32_t lane = threadIdx.x & 63;
-        /* step m: DMA step m+2 into the tile step m-1 used, wait for step m's
-           four loads (8 newer ones may stay in flight), Poly over the unit */
-        auto step = [&](uint32_t m, const uint4 *cur, uint4 *nxt) {
-            auth_dma<K>(rv, g, k, m + 2, nxt);
-            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            /* the tile is read by hand: the compiler cannot tell which tile an
-               LDS-DMA fills and would wait for all of them (vmcnt(0)) */
-            uint32_t w[16];
-            const uint32_t addr = (uint32_t)(uintptr_t)(const lds_void *)(cur + lane);
-            uint4 q0, q1, q2, q3;
-            asm volatile("ds_read_b128 %0, %4\n"
-                         "ds_read_b128 %1, %4 offset:1024\n"
-                         "ds_read_b128 %2, %4 offset:2048\n"
-                         "ds_read_b128 %3, %4 offset:3072\n"
-                         "s_waitcnt lgkmcnt(0)"
-                         : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3) : "v"(addr) : "memory");
-            w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w;
-            w[4] = q1.x; w[5] = q1.y; w[6] = q1.z; w[7] = q1.w;
-            w[8] = q2.x; w[9] = q2.y; w[10] = q2.z; w[11] = q2.w;
-            w[12] = q3.x; w[13] = q3.y; w[14] = q3.z; w[15] = q3.w;
-            const int v = (int)(m * K + (uint32_t)k) - (int)g.o;
-            if (v >= 1) {
-                const uint32_t j = (uint32_t)v - 1;
-                uint32_t nb = 4;
-                if (j + 1 == g.J) {
-                    const uint32_t bytes = len - 64 * j;
-                    mask_unit(w, bytes);
-                    nb = (bytes + 15) / 16;
-                }
-                poly_unit(acc, seen ? mjump : mr, mr, w, nb);
-                seen = true;
-            }
-            __builtin_amdgcn_wave_barrier(); /* all lanes read cur before it is refilled */
-        };
-        auth_dma<K>(rv, g, k, 0, ring.t0);
-        auth_dma<K>(rv, g, k, 1, ring.t1);
-        for (uint32_t m = 0; m < g.steps; m += 3) {
-            step(m, ring.t0, ring.t2);
-            if (m + 1 < g.steps) step(m + 1, ring.t1, ring.t0);
-            if (m + 2 < g.steps) step(m + 2, ring.t2, ring.t1);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* no DMA outlives the pass */
-    } else {
 #pragma unroll
     for (int i = 0; i < 16; ++i) wn[i] = 0;
     unit_prefetch<FAST>(rv.src, v0 >= 1, (uint32_t)v0 - 1, len, wn);
@@ -658,7 +590,6 @@ NA_DEV bool open_il(const RecView &rv, int k, AuthRing ring = AuthRing{})
             poly_unit(acc, seen ? mjump : mr, mr, wc, nb);
             seen = true;
         }
-    }
     }
     uint32_t tag[4], got[4];
     if (tree) poly_tree_close<K>(acc, k, r, mr, g.J, g.q, rv.ad_len, len, s, tag);
@@ -809,16 +740,12 @@ NA_DEV void wave_dma(const UniformArgs &a, const WaveIO<K> &io, int j0, uint4 *t
    the written lines need not displace the ciphertext lines the next step of
    an open still reads.  Round 4: the 4-lane kernels' standalone C2 seal+open
    +1.0-1.9 % in three interleaved rounds, C5 unchanged
-   (profiles/r04/nt_store_ab.jsonl); NA_PLAIN_STORE restores plain stores. */
+   (profiles/r04/nt_store_ab.jsonl). */
 typedef uint32_t na_u32x4 __attribute__((ext_vector_type(4)));
 NA_DEV void rec_store16(uint8_t *p, const uint4 &q)
 {
-#ifndef NA_PLAIN_STORE
     na_u32x4 v = {q.x, q.y, q.z, q.w};
     __builtin_nontemporal_store(v, (na_u32x4 *)p);
-#else
-    *(uint4 *)p = q;
-#endif
 }
 
 /* Coalesced stores of the step's full units (unit <= last_full) from the
@@ -828,28 +755,13 @@ NA_DEV void wave_store(const UniformArgs &a, const WaveIO<K> &io, int j0, int la
                        const uint4 *t, uint32_t lane, uint32_t okm)
 {
     const int u = j0 + io.kk;
-#ifdef NA_STORE_AUX
-    /* buffer stores with cache-policy bits NA_STORE_AUX (sc0 = 1, nt = 2,
-       sc1 = 16) from the wave's first record (A/B builds) */
-    const uint32_t r0 = __builtin_amdgcn_readfirstlane(io.rq);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        a.out + (size_t)r0 * a.out_stride, 0, 0x7FFFFFFF, 0x00020000);
-#endif
     if (u < 0 || u > last_full) return;
     const uint32_t off = io.c16 + 64u * (uint32_t)u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint4 q = t[tile_slot(16u * i + (lane >> 2), lane & 3)];
         const uint32_t r = wave_rec(io, i);
-        if (r < a.n_records && ((okm >> i) & 1)) {
-#ifdef NA_STORE_AUX
-            const na_u32x4 v = {q.x, q.y, q.z, q.w};
-            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r - r0) * (uint32_t)a.out_stride + off, 0,
-                                                   NA_STORE_AUX);
-#else
-            rec_store16(a.out + (size_t)r * a.out_stride + off, q);
-#endif
-        }
+        if (r < a.n_records && ((okm >> i) & 1)) rec_store16(a.out + (size_t)r * a.out_stride + off, q);
     }
 }
 
@@ -1158,13 +1070,8 @@ NA_DEV uint32_t solo_chunk(uint32_t lane) { return (lane ^ (lane >> 3)) & 7; }
 NA_DEV void dma16_asm(const void *g, uint32_t lds)
 {
     uint32_t keep;
-#ifdef NA_DMA_NT
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-#else
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-#endif
 }
 
 /* every vector-memory operation of the wave done (the DMA into the tile
@@ -1283,18 +1190,38 @@ NA_DEV SoloRec solo_rec(const UniformArgs &a, uint32_t wave_job)
    (hipcc waits before an LDS read for the youngest LDS-DMA; reading the tile
    after issuing the next DMA, as the 4-lane kernels do, made every step wait
    for the DMA it had just issued and serialised the stores behind it.) */
-/* solo_pass modes: SEAL and OPEN1 (one-pass open) as above; the
-   verify-first open runs solo_auth (below) and then DEC over the verified
-   records (key stream only; stores gated by okm, the owners' verdicts per
-   coalesced instruction, and ok). */
-enum SoloMode { SOLO_SEAL, SOLO_OPEN1, SOLO_DEC };
+/* The key stream of a one-lane step (blocks c0, c0 + 1 of the lane's
+   record).  NA_CHACHA_RUNS (round-6 A/B): 0 = chacha20_block_pre per block
+   (hipcc's schedule); 1 = the two blocks in lock step issued in runs
+   (chacha20_2block_runs) without priority toggles; 2 = rotate runs at
+   s_setprio 2, fast runs at 0; 3 = 3 / 1. */
+#ifndef NA_CHACHA_RUNS
+#define NA_CHACHA_RUNS 0
+#endif
+#if NA_CHACHA_RUNS
+NA_DEV void solo_blocks2(const uint32_t key[8], const ChaPre &pre, uint32_t c0, uint32_t n_lo, uint32_t n_hi,
+                         uint32_t (&x0)[16], uint32_t (&x1)[16])
+{
+#if NA_CHACHA_RUNS == 1
+    chacha20_2block_runs<-1, -1, -1>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
+#elif NA_CHACHA_RUNS == 2
+    chacha20_2block_runs<2, 0, 0>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
+#else
+    chacha20_2block_runs<3, 1, 1>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
+#endif
+}
+#endif
+
+/* solo_pass modes: SEAL and OPEN1 (the opt-in one-pass open,
+   NOISE_AEAD_FLAG_ONE_PASS) as above; the verify-first open (the default)
+   runs solo_auth and then solo_dec_rev (below). */
+enum SoloMode { SOLO_SEAL, SOLO_OPEN1 };
 
 template <int MODE>
 NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const uint32_t key[8],
-                      const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, const R32 &r, P32 &h,
-                      uint32_t okm = 0xffu, bool ok = true)
+                      const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, const R32 &r, P32 &h)
 {
-    constexpr bool POLY = MODE != SOLO_DEC;
+    constexpr uint32_t okm = 0xffu;
     for (uint32_t m = 0; m < q.S; ++m) {
         uint4 *cur = tiles + SOLO_TILE * (m & 1), *nxt = tiles + SOLO_TILE * ((m + 1) & 1);
         uint32_t wu[2][16];
@@ -1310,12 +1237,21 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
            ahead lowers its priority (aead_device.h): C2 +5-8 %, C4 +0.5 %
            (profiles/r04/solo_prio_ab.jsonl). */
         prio_by_progress(m, q.S);
+#if NA_CHACHA_RUNS
+        uint32_t xs[2][16];
+        solo_blocks2(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1]);
+#endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u; /* unit, ChaCha block j + 1 */
             if (j < q.J) {
                 uint32_t x[16], w[16];
+#if NA_CHACHA_RUNS
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
+#else
                 chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+#endif
                 uint32_t nb = 4;
                 if constexpr (MODE == SOLO_OPEN1) {
 #pragma unroll
@@ -1332,13 +1268,11 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
 #pragma unroll
                     for (int i = 0; i < 16; ++i) w[i] = wu[u][i] ^ x[i];
                     if (j == q.J - 1) {
-                        if (q.live && ok) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
-                        if (POLY) {
-                            mask_unit(w, q.tail);
-                            nb = (q.tail + 15) / 16;
-                        }
+                        if (q.live) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
+                        mask_unit(w, q.tail);
+                        nb = (q.tail + 15) / 16;
                     }
-                    if constexpr (POLY) p32_unit(h, r, w, nb);
+                    p32_unit(h, r, w, nb);
                 }
                 solo_put(cur, q.lane, u, w);
             }
@@ -1390,9 +1324,7 @@ NA_DEV void solo_auth(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the tile is read before the DMA refills it */
         __builtin_amdgcn_wave_barrier();
         if (m + 2 < q.S) solo_dma(a, q.rec0, q.lane, m + 2, q.lim, cur);
-#ifndef NA_SOLO_NO_AUTH_PRIO
         __builtin_amdgcn_s_setprio(3);
-#endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u;
@@ -1408,21 +1340,18 @@ NA_DEV void solo_auth(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
     }
 }
 
-/* The verify-first open's DEC pass from the last step back to the first
-   (NA_DEC_REV): key-stream blocks are independent of each other, and the
-   AUTH pass leaves steps S-1 and S-2 in the two tiles (it refills a tile
-   with step m+2 only while m+2 < S), so those two are decrypted without
-   reading them again and the pass starts without a DMA wait.  Otherwise
-   solo_pass<SOLO_DEC> with the step order reversed: the wait, the read of
-   step m, the store of step m+1's output from the other tile, the DMA of
-   step m-1 into it, the key stream into this tile.  C2 --verify-first
-   1396-1431 -> 1460-1468 GiB/s, three interleaved rounds
-   (profiles/r05/dec_rev_ab.txt); the last steps read by the AUTH pass are
-   also the likeliest still in L2.  NA_DEC_REV=0: the forward pass (A/B). */
-#ifndef NA_DEC_REV
-#define NA_DEC_REV 1
-#endif
-#if NA_DEC_REV
+/* The verify-first open's DEC pass from the last step back to the first:
+   key-stream blocks are independent of each other, and the AUTH pass leaves
+   steps S-1 and S-2 in the two tiles (it refills a tile with step m+2 only
+   while m+2 < S), so those two are decrypted without reading them again and
+   the pass starts without a DMA wait.  Per step: the wait, the read of step
+   m, the store of step m+1's output from the other tile (gated by okm, the
+   owners' verdicts per coalesced instruction), the DMA of step m-1 into it,
+   the key stream into this tile.  Round 5 measured it against the forward
+   order: C2 verify-first 1396-1431 -> 1460-1468 GiB/s, three interleaved
+   rounds (profiles/r05/dec_rev_ab.txt; the forward pass is NA_DEC_REV=0 at
+   the ab-arms-r5 revision, tools/ab/README.md); the last steps read by the
+   AUTH pass are also the likeliest still in L2. */
 NA_DEV void solo_dec_rev(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const uint32_t key[8],
                          const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, uint32_t okm, bool ok)
 {
@@ -1437,12 +1366,21 @@ NA_DEV void solo_dec_rev(const UniformArgs &a, const SoloRec &q, uint4 *tiles, c
         __builtin_amdgcn_wave_barrier();
         if (k >= 1 && m >= 1) solo_dma(a, q.rec0, q.lane, m - 1, q.lim, nxt); /* k = 0: step S-2 is there */
         prio_by_progress(k, q.S);
+#if NA_CHACHA_RUNS
+        uint32_t xs[2][16];
+        solo_blocks2(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1]);
+#endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u;
             if (j < q.J) {
                 uint32_t x[16], w[16];
+#if NA_CHACHA_RUNS
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
+#else
                 chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+#endif
 #pragma unroll
                 for (int i = 0; i < 16; ++i) w[i] = wu[u][i] ^ x[i];
                 if (j == q.J - 1 && q.live && ok) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
@@ -1455,79 +1393,16 @@ NA_DEV void solo_dec_rev(const UniformArgs &a, const SoloRec &q, uint4 *tiles, c
         solo_store(a, q.rec0, q.lane, 0, q.full_lim, tiles, okm);
     }
 }
-#endif
 
-/* The AUTH pass with the ciphertext loaded straight into registers instead
-   of through the LDS tiles: each lane reads its own record's 128-B step with
-   eight 16-B loads (whole 128-B lines), D steps in flight (D x 32 VGPRs,
-   free during this pass: the kernel's allocation is set by the ChaCha
-   passes).  The tiles' two steps in flight left the pass latency-bound —
-   ~50 us of a ~120 us C2 verify-first duplex launch
-   (profiles/r04/timeline/timeline_solo.txt) during which the SIMD's other
-   wave issued alone.  Measured slower (profiles/r05/auth_reg_ab.txt: C2
-   verify-first 1412-1428 GiB/s at D = 2, 3, 4, 6 against 1462-1464 through
-   the tiles; one pass 1626-1629): the per-lane loads touch 64 lines per
-   instruction where the tile DMA moves 8 whole 128-B runs.  Kept as the
-   A/B (NA_AUTH_REG=D); the default is the tile pass (0). */
-#ifndef NA_AUTH_REG
-#define NA_AUTH_REG 0
-#endif
-#if NA_AUTH_REG
-template <int D>
-NA_DEV void solo_auth_reg(const UniformArgs &a, const SoloRec &q, const R32 &r, P32 &h)
-{
-    const uint8_t *src = u_src(a, q.rc);
-    uint4 buf[D][8];
-    /* step m's 8 chunks; chunks at or past lim (64 J: readable in a FAST
-       slot) re-read the record's first chunk and are never used */
-    auto load = [&](uint4 *b, uint32_t m) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            uint32_t off = 128u * m + 16u * (uint32_t)i;
-            if (off >= q.lim) off = 0;
-            b[i] = *(const uint4 *)(src + off);
-        }
-    };
-#pragma unroll
-    for (int d = 0; d < D; ++d) load(buf[d], (uint32_t)d);
-    for (uint32_t m0 = 0; m0 < q.S; m0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const uint32_t m = m0 + (uint32_t)d;
-            if (m < q.S) {
-                __builtin_amdgcn_s_setprio(3);
-#pragma unroll
-                for (uint32_t u = 0; u < 2; ++u) {
-                    const uint32_t j = 2 * m + u;
-                    if (j < q.J) {
-                        uint32_t w[16];
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            const uint4 v = buf[d][4 * u + c];
-                            w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-                        }
-                        uint32_t nb = 4;
-                        if (j == q.J - 1) {
-                            mask_unit(w, q.tail);
-                            nb = (q.tail + 15) / 16;
-                        }
-                        p32_unit(h, r, w, nb);
-                    }
-                }
-                if (m + D < q.S) load(buf[d], m + D);
-            }
-        }
-    }
-}
-#endif
 
-/* Open, one pass: Poly1305 over each ciphertext unit as it arrives, then
-   the plaintext out; a wave holding a rejected record repairs it after the
-   verdict exactly as open_il_staged does (in place: XOR with the key stream
-   once more; out of place: zeroed).  VERIFY_FIRST (a.vf, the reference's
-   order, cipher-chachapoly.c:135-141): an AUTH pass over the wave's records,
-   the verdicts, then a DEC pass writing only verified records — a rejected
-   record's output is never written.  The DEC pass reads the ciphertext
+/* Open.  Verify-first (a.vf: the default, the reference's order,
+   cipher-chachapoly.c:135-141): an AUTH pass over the wave's records, the
+   verdicts, then a DEC pass writing only verified records — a rejected
+   record's output is never written.  One pass (NOISE_AEAD_FLAG_ONE_PASS):
+   Poly1305 over each ciphertext unit as it arrives, then the plaintext out;
+   a wave holding a rejected record repairs it after the verdict exactly as
+   open_il_staged does (in place: XOR with the key stream once more; out of
+   place: zeroed).  The DEC pass reads the ciphertext
    again, mostly from L2 / MALL (a wave's 64 records are ~90 KB). */
 template <bool UKEY>
 NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_job)
@@ -1540,20 +1415,12 @@ NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
     u_key_nonce<UKEY>(a, rec0, rc, key, n_lo, n_hi);
     ChaPre pre;
     chacha_pre(key, n_lo, n_hi, pre);
-#if NA_AUTH_REG
-    if (S && !a.vf) solo_dma(a, rec0, lane, 0, lim, tiles);
-#else
     if (S) solo_dma(a, rec0, lane, 0, lim, tiles);
-#endif
     R32 r;
     uint32_t s[4];
     P32 h;
     solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, rc) : nullptr, a.ad_len, r, s, h);
-#if NA_AUTH_REG
-    if (a.vf) solo_auth_reg<NA_AUTH_REG>(a, q, r, h);
-#else
     if (a.vf) solo_auth(a, q, tiles, r, h);
-#endif
     else solo_pass<SOLO_OPEN1>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
     uint32_t tag[4], got[4];
     solo_tag(h, r, a.ad_len, len, s, tag);
@@ -1571,12 +1438,7 @@ NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
         for (int i = 0; i < 8; ++i)
             okm |= (__shfl((int)ok, (int)(8u * i + (lane >> 3)), 64) != 0 ? 1u : 0u) << i;
         __builtin_amdgcn_wave_barrier(); /* the AUTH pass's tile reads are done */
-#if NA_DEC_REV && !NA_AUTH_REG
         solo_dec_rev(a, q, tiles, key, pre, n_lo, n_hi, okm, ok);
-#else
-        if (S) solo_dma(a, rec0, lane, 0, lim, tiles);
-        solo_pass<SOLO_DEC>(a, q, tiles, key, pre, n_lo, n_hi, r, h, okm, ok);
-#endif
         return;
     }
     const bool bad = live && !ok;
@@ -1809,9 +1671,7 @@ NA_DEV bool open_ct(const RecView &rv, int k)
 
 /* 4 waves per SIMD: one C2-sized batch (64 Ki records, 4 lanes each) is then
    exactly one resident round of the 1024 SIMDs */
-#ifndef NA_UNIFORM_OCC
 #define NA_UNIFORM_OCC __attribute__((amdgpu_waves_per_eu(4)))
-#endif
 
 /* lanes per record: 1 or 2 -> contiguous runs, 4 .. 64 -> interleaved units */
 template <int K, bool FAST>
@@ -1904,56 +1764,6 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_staged(
     else seal_il_staged<K, UKEY>(s, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], wave_of(b));
 }
 
-#ifdef NA_AB_KERNELS /* measured slower (profiles/r03/persist_ab); A/B variant builds only */
-/* Persistent duplex: the same two jobs as chachapoly_duplex_staged, but a grid
-   of at most the resident workgroups (4 per CU) whose waves take wave-jobs
-   (64/K records of one job) from a ticket counter until none are left:
-   tickets alternate seal / open while both jobs have some, then the longer
-   job's remainder.  A wave goes on to its next wave-job as soon as it
-   finishes one — no workgroup waits for its slowest wave and no second
-   generation is dispatched — and a faster SIMD simply takes more wave-jobs,
-   so every SIMD keeps four waves until the tickets run out.  Each wave-job
-   runs exactly the code of the separate kernels, so results are identical.
-   ctr[0] hands out tickets, ctr[1] counts finished waves; the last wave to
-   finish resets both, so the next launch on the stream starts from zero
-   (stream order; the library keeps one counter pair per stream). */
-template <int K, bool UKEY>
-__global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_persist(
-    UniformArgs s, UniformArgs o, uint32_t s_jobs, uint32_t o_jobs, uint32_t *ctr)
-{
-    __shared__ uint4 tiles[4][512];
-    __shared__ FinSlot fin[4];
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t n = min(s_jobs, o_jobs), total = s_jobs + o_jobs;
-    for (;;) {
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd(&ctr[0], 1u);
-        t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)t, 0, 64));
-        if (t >= total) break; /* every wave draws exactly one ticket past the end */
-        bool open;
-        uint32_t j;
-        if (t < 2 * n) {
-            open = t & 1;
-            j = t >> 1;
-        } else {
-            open = o_jobs > s_jobs;
-            j = t - n;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (open) open_il_staged<K, UKEY>(o, tiles[w], &fin[w], j);
-        else seal_il_staged<K, UKEY>(s, tiles[w], &fin[w], j);
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (lane == 0) {
-        const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-        if (atomicAdd(&ctr[1], 1u) == waves - 1) { /* every wave has drawn its last ticket */
-            atomicExch(&ctr[0], 0u);
-            atomicExch(&ctr[1], 0u);
-        }
-    }
-}
-
-#endif
 
 /* One lane per record (seal_solo_staged): two waves per SIMD, 16 KB of LDS
    each; 256 records per workgroup. */
@@ -2056,18 +1866,9 @@ __global__ __launch_bounds__(256) void chachapoly_open_ragged(RaggedArgs a)
     const RecView rv = ragged_view(a, rec);
     if (reject_len(a, rec, rv.len, k == K - 1)) return;
     bool ok;
-#ifdef NA_RAGGED_OPEN_RING
-    if constexpr (FAST && K >= 4) {
-        __shared__ uint4 r0[4][256], r1[4][256], r2[4][256]; /* 3 x 4 KB per wave */
-        const uint32_t w = threadIdx.x >> 6;
-        ok = open_il<K, true, true>(rv, k, AuthRing{r0[w], r1[w], r2[w]});
-    } else
-#else
     if constexpr (FAST && K >= 4 && !VF) {
         ok = open_il_1p<K>(rv, k); /* one pass: the ciphertext is read once */
-    } else
-#endif
-    {
+    } else {
         ok = open_any<K, FAST>(rv, k);
     }
     if (k == K - 1 && a.status) a.status[rec] = ok ? 0 : 1;

@@ -95,11 +95,9 @@ struct SegTL {
 #endif
 
 /* Blocks per lane a ragged record aims at (K = the smallest power of two with
-   ceil(B/K) <= SEG_TARGET, at most SEG_KMAX) */
-#ifndef NA_SEG_TARGET
-#define NA_SEG_TARGET 32
-#endif
-constexpr uint32_t SEG_TARGET = NA_SEG_TARGET;
+   ceil(B/K) <= SEG_TARGET, at most SEG_KMAX; 24/32/48/64 measured, 32 the
+   fastest, profiles/r05/) */
+constexpr uint32_t SEG_TARGET = 32;
 constexpr uint32_t SEG_KMAX = 16;
 constexpr uint32_t SEG_BUCKETS = 1025; /* J = 0 .. 1024 (65519-byte records) */
 
@@ -205,9 +203,6 @@ NA_DEV void seg_store16(uint64_t a, const uint4 &q)
     __builtin_nontemporal_store(v, (seg_gvec *)(uintptr_t)a);
 }
 
-#ifndef NA_SEG_INTERIOR
-#define NA_SEG_INTERIOR 1
-#endif
 struct SegIOL {
     SegOwner *tab; /* this wave's 64 owners (LDS) */
     /* wave-uniform: the smallest readable end and store limit over the
@@ -233,7 +228,7 @@ struct SegIOL {
     {
         const uint32_t c = solo_chunk(lane);
         const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)t);
-        if (NA_SEG_INTERIOR && m >= 1 && 128u * m + 128u <= min_hi) { /* interior step (wave-uniform) */
+        if (m >= 1 && 128u * m + 128u <= min_hi) { /* interior step (wave-uniform) */
             const uint32_t off = 128u * m + 16u * c;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -256,7 +251,7 @@ struct SegIOL {
         /* the tile values and owner entries first, one wait, then the stores
            (a read and its wait inside each store's branch serialised them) */
         const uint32_t off = 128u * m + 16u * solo_chunk(lane);
-        const bool interior = NA_SEG_INTERIOR && m >= 1 && 128u * m + 128u <= min_sl; /* wave-uniform */
+        const bool interior = m >= 1 && 128u * m + 128u <= min_sl; /* wave-uniform */
         uint4 v[8];
         uint64_t dst[8];
         uint32_t ok = 0;
@@ -607,15 +602,21 @@ NA_DEV uint32_t seg_owner_mask(bool f, uint32_t lane)
 
 /* A one-pass open's repair of rejected records' segments (in place: the
    plaintext XORed with the key stream again; out of place: zeroed), over
-   the same coalesced stores, gated by badm. */
+   the same coalesced stores, gated by badm.  `inplace` is per lane (a
+   ragged batch may mix in-place and out-of-place records), but lane l's DMA
+   chunk belongs to owner 8i + l/8, not to lane l's record: the DMA runs on
+   every lane whenever any lane of the wave is in place (an out-of-place
+   owner's chunks are read and not used), so each in-place owner's tile is
+   filled whatever its neighbours are. */
 template <class IO>
 NA_DEV void seg_repair(const SegLane &q, const IO &io, uint32_t lane, uint32_t S, uint4 *tiles,
                        const uint32_t key[8], const ChaPre &pre, bool bad, uint32_t badm, bool inplace)
 {
+    const bool any_inplace = __ballot(inplace) != 0; /* wave-uniform */
     __threadfence(); /* this wave's plaintext stores, visible to its reads below */
     for (uint32_t m = 0; m < S; ++m) {
         __builtin_amdgcn_wave_barrier();
-        if (inplace) {
+        if (any_inplace) {
             /* the DMA reads the output (in place: the same bytes) */
             io.dma(lane, m, tiles);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -887,12 +888,9 @@ NA_DEV SegLane seg_ragged_lane(const RaggedArgs &a, uint32_t e, uint32_t e0, uin
     return q;
 }
 
-/* Persistent: 2 workgroups per CU, each wave taking jobs from the ticket.
-   NA_SEG_PREFETCH (default 1): the next job's ticket and plan entries are
-   taken as the current job's data pass ends; 0: at the top of the loop. */
-#ifndef NA_SEG_PREFETCH
-#define NA_SEG_PREFETCH 1
-#endif
+/* Persistent: 2 workgroups per CU, each wave taking jobs from the ticket;
+   the next job's ticket and plan entries are taken as the current job's
+   data pass ends (below). */
 template <bool OPEN>
 __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seg_ragged(RaggedArgs a, SegPlanHdr *p,
                                                                          const uint32_t *map)
@@ -923,14 +921,9 @@ __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seg_ragged(RaggedA
         t = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tn, 0, 64));
         seg_map_entries(map, total, n_jobs, t, lane, e_nx, e0_nx);
     };
-#if NA_SEG_PREFETCH
     next();
-#endif
     for (;;) {
         const uint64_t t0 = SegTL::now();
-#if !NA_SEG_PREFETCH
-        next();
-#endif
         if (t >= n_jobs) break; /* every wave draws one ticket past the end */
         const uint32_t e = e_nx, e0 = e0_nx;
         uint32_t key[8];
@@ -941,11 +934,7 @@ __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seg_ragged(RaggedA
         io.init(q, lane);
         const bool inplace = q.src == q.dst;
         tl.add(1, SegTL::now() - t0);
-#if NA_SEG_PREFETCH
         seg_job<OPEN, false>(q, key, io, lane, tiles[w], a.status, a.vf != 0, inplace, tl, next);
-#else
-        seg_job<OPEN, false>(q, key, io, lane, tiles[w], a.status, a.vf != 0, inplace, tl);
-#endif
         const uint64_t td = SegTL::now();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); /* the job's stores left before the tile is reused */
         __builtin_amdgcn_wave_barrier();

@@ -105,48 +105,10 @@ int aes_prepare(const uint8_t *raw_keys, uint32_t n_states, void *ctx, hipStream
     return hip_rc(hipGetLastError());
 }
 
-#ifdef NA_AB_KERNELS
-/* NOISE_AEAD_GCM_BS=1: uniform FAST jobs without AD whose states cover
-   whole 128-record workgroups take the bitsliced-AES kernels (aesgcm.hip
-   gcm_bs_*: constant-time AES, table GHASH) — the round-4 A/B of the
-   T-table design; =2: the 1024-thread variant with an 8-bit
-   multiply-by-H table (512-record workgroups). */
-static int gcm_bs_mode()
-{
-    static const int v = [] {
-        const char *e = getenv("NOISE_AEAD_GCM_BS");
-        return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
-    }();
-    return v;
-}
-
-static uint32_t gcm_bs_recs() { return gcm_bs_mode() == 2 ? GCM_BS8_RECS : GCM_BS_RECS; }
-
-/* seals only: every AES-GCM open verifies first (aead_api.hip open_vf),
-   which the bitsliced open kernels do not implement */
-static bool gcm_bs_fits(const UniformArgs &a, bool ct)
-{
-    return gcm_bs_mode() && !ct && !a.vf && a.ad_len == 0 && a.rps % gcm_bs_recs() == 0;
-}
-
-#endif
 
 int aes_uniform(const UniformArgs &a, bool open, bool ct, bool staged, hipStream_t s)
 {
     if (a.n_records == 0) return NOISE_ERROR_NONE;
-#ifdef NA_AB_KERNELS
-    if (staged && gcm_bs_fits(a, ct)) {
-        const uint32_t R = gcm_bs_recs(), blocks = (a.n_records + R - 1) / R;
-        if (R == GCM_BS8_RECS) {
-            worker_park_for_batch(blocks);
-            hipLaunchKernelGGL(open ? gcm_bs8_uniform<true> : gcm_bs8_uniform<false>, dim3(blocks), dim3(1024), 0, s, a);
-        } else {
-            worker_park_for_batch(blocks / 4);
-            hipLaunchKernelGGL(open ? gcm_bs_uniform<true> : gcm_bs_uniform<false>, dim3(blocks), dim3(256), 0, s, a);
-        }
-        return hip_rc(hipGetLastError());
-    }
-#endif
     if (staged) { /* one state per 256-record workgroup + FAST layout */
         const uint32_t blocks = (a.n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
         worker_park_for_batch(blocks);
@@ -178,20 +140,6 @@ static bool gcm_duplex_fused_on()
 
 int aes_duplex(const UniformArgs &a, const UniformArgs &b, bool ct, hipStream_t s)
 {
-#ifdef NA_AB_KERNELS
-    if (gcm_bs_fits(a, ct) && gcm_bs_fits(b, ct)) {
-        const uint32_t R = gcm_bs_recs();
-        const uint32_t sb = (a.n_records + R - 1) / R, ob = (b.n_records + R - 1) / R;
-        if (R == GCM_BS8_RECS) {
-            worker_park_for_batch(sb + ob);
-            hipLaunchKernelGGL((gcm_bs_duplex<1024, true>), dim3(sb + ob), dim3(1024), 0, s, a, b, sb, ob);
-        } else {
-            worker_park_for_batch((sb + ob) / 4);
-            hipLaunchKernelGGL((gcm_bs_duplex<256, false>), dim3(sb + ob), dim3(256), 0, s, a, b, sb, ob);
-        }
-        return hip_rc(hipGetLastError());
-    }
-#endif
     const uint32_t sb = (a.n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
     const uint32_t ob = (b.n_records + GCM_WG_RECS - 1) / GCM_WG_RECS;
     worker_park_for_batch(sb > ob ? sb : ob);

@@ -7,10 +7,9 @@
 #include "launch.h"
 #include "chachapoly.hip"
 #include "chachapoly_seg.hip"
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
-#include <map>
-#include <mutex>
 
 namespace na {
 namespace {
@@ -106,56 +105,6 @@ uint32_t resident_blocks(F fn)
     return (uint32_t)(cus * per);
 }
 
-#ifdef NA_AB_KERNELS
-/* The ticket counter pair of chachapoly_duplex_persist for (device, stream):
-   zeroed once, stream-ordered before the first launch; each launch leaves it
-   zeroed for the next one on the same stream. */
-std::mutex g_ctr_mu;
-std::map<std::pair<int, hipStream_t>, uint32_t *> g_ctr;
-
-uint32_t *ticket_counter(hipStream_t s)
-{
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_ctr_mu);
-    uint32_t *&c = g_ctr[{dev, s}];
-    if (!c) {
-        if (hipMalloc((void **)&c, 64) != hipSuccess) {
-            c = nullptr;
-            return nullptr;
-        }
-        if (hipMemsetAsync(c, 0, 64, s) != hipSuccess) return nullptr;
-    }
-    return c;
-}
-
-/* NOISE_AEAD_DUPLEX=persist | plain selects the duplex kernel (A/B runs). */
-bool duplex_persist()
-{
-    static const int v = [] {
-        const char *e = getenv("NOISE_AEAD_DUPLEX");
-        return e && !strcmp(e, "persist") ? 1 : 0;
-    }();
-    return v != 0;
-}
-
-template <int K, bool UKEY>
-int duplex_persist_launch(const UniformArgs &a, const UniformArgs &b, hipStream_t s)
-{
-    auto fn = chachapoly_duplex_persist<K, UKEY>;
-    static uint32_t resident = 0; /* one device model per process: MI355X */
-    if (!resident) resident = resident_blocks(fn);
-    uint32_t *ctr = ticket_counter(s);
-    if (!resident || !ctr) return NOISE_ERROR_SYSTEM;
-    const uint32_t sj = (uint32_t)(((uint64_t)a.n_records * K + 63) / 64);
-    const uint32_t oj = (uint32_t)(((uint64_t)b.n_records * K + 63) / 64);
-    const uint32_t want = (sj + oj + 3) / 4;
-    worker_park_for_batch(want);
-    hipLaunchKernelGGL(fn, dim3(want < resident ? want : resident), dim3(256), 0, s, a, b, sj, oj, ctr);
-    return hip_rc(hipGetLastError());
-}
-
-#endif
 
 } // namespace
 
@@ -192,13 +141,6 @@ static uint32_t duplex_run_chunk()
 
 int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, hipStream_t s)
 {
-#ifdef NA_AB_KERNELS
-    if (duplex_persist() && k != 1) {
-        if (k == 4) return ukey ? duplex_persist_launch<4, true>(a, b, s) : duplex_persist_launch<4, false>(a, b, s);
-        if (k == 8) return ukey ? duplex_persist_launch<8, true>(a, b, s) : duplex_persist_launch<8, false>(a, b, s);
-        return NOISE_ERROR_INVALID_PARAM;
-    }
-#endif
     const uint32_t sb = (uint32_t)(((uint64_t)a.n_records * k + 255) / 256);
     const uint32_t ob = (uint32_t)(((uint64_t)b.n_records * k + 255) / 256);
     if (k == 1) {
@@ -221,6 +163,26 @@ int chacha_ragged(const RaggedArgs &a, int k, bool open, bool fast, hipStream_t 
     KernelFn<RaggedArgs> fn = chacha_ragged_fn(k, open, fast, a.vf != 0);
     if (!fn) return NOISE_ERROR_INVALID_PARAM;
     return launch(fn, a.n_records, k, a, s);
+}
+
+/* Resident workgroups of chachapoly_seg_ragged<open> on the current device,
+   cached per device (a host may mix GPU models): the persistent
+   grid and worker_park_for_batch take this count. */
+template <typename F>
+uint32_t seg_resident(bool open, F fn)
+{
+    constexpr int MAX_DEV = 64;
+    static std::atomic<uint32_t> cache[MAX_DEV][2];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+    if (dev >= MAX_DEV) return resident_blocks(fn);
+    std::atomic<uint32_t> &c = cache[dev][open ? 1 : 0];
+    uint32_t v = c.load(std::memory_order_relaxed);
+    if (!v) {
+        v = resident_blocks(fn); /* idempotent: a racing thread stores the same value */
+        c.store(v, std::memory_order_relaxed);
+    }
+    return v;
 }
 
 /* Ragged FAST batch through the segmented one-lane kernel: the plan (count,
@@ -251,9 +213,7 @@ int chacha_ragged_seg(const RaggedArgs &a, bool open, hipStream_t s)
     }
     if (!rc) {
         auto fn = open ? chachapoly_seg_ragged<true> : chachapoly_seg_ragged<false>;
-        static uint32_t resident[2] = {0, 0}; /* one device model per process: MI355X */
-        uint32_t &res = resident[open ? 1 : 0];
-        if (!res) res = resident_blocks(fn);
+        const uint32_t res = seg_resident(open, fn);
         const uint64_t most = ((uint64_t)a.n_records * SEG_KMAX + 255) / 256; /* jobs / 4, at most */
         const uint32_t grid = (uint32_t)(res && most > res ? res : (most ? most : 1));
         if (!res) rc = NOISE_ERROR_SYSTEM;

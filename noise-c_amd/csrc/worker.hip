@@ -523,10 +523,7 @@ NA_DEV uint4 load_sys16_raw(const uint8_t *p)
 }
 
 /* polls without a request after which only the header is polled: 20 us */
-#ifndef NA_POLL_BACKOFF
-#define NA_POLL_BACKOFF 2000
-#endif
-constexpr uint64_t POLL_BACKOFF = NA_POLL_BACKOFF;
+constexpr uint64_t POLL_BACKOFF = 2000;
 
 /* A worker GROUP is one kernel of nslots workgroups on one high-priority
    stream, workgroup i serving request slot i: several calling threads per
@@ -1134,6 +1131,19 @@ bool debug_launch_fails()
     return v;
 }
 
+/* Test hook: NOISE_AEAD_DEBUG_WORKER_LEAVE=1 makes the group leave after a
+   call has checked it is up and before it posts its request, so the wait
+   loop must relaunch it (the mid-wait relaunch of ADVICE r5,
+   tests/worker_mode_check.py --relaunch-free). */
+bool debug_leave_before_post()
+{
+    static const bool v = [] {
+        const char *e = getenv("NOISE_AEAD_DEBUG_WORKER_LEAVE");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 /* NOISE_AEAD_WORKER_PARK=0: batch launches leave the workers resident (the
    A/B of tests/test_gpu_worker.py's batch-beside-worker measurement). */
 bool park_enabled()
@@ -1368,6 +1378,13 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
     /* after the launch (which starts the history afresh): this context may
        now sit in the workgroup's LDS cache */
     if (h_ctx) worker_note_ctx(w, h_ctx);
+    if (debug_leave_before_post()) { /* test hook: the group leaves before k is posted */
+        park_group(g);
+        const uint64_t t0 = host_ns();
+        while ((!__atomic_load_n(&s->exiting, __ATOMIC_ACQUIRE) || hipStreamQuery(g.stream) != hipSuccess) &&
+               host_ns() - t0 < 1000000000ull)
+            __builtin_ia32_pause();
+    }
     const uint32_t k = ++w.seq;
     /* the input stream key || AD || pad || record (|| tag): its first head
        bytes as stamped chunks, the rest raw.  Host memory: 12 stream bytes +
@@ -1438,6 +1455,11 @@ extern "C" NA_HIDDEN int na_worker_crypt(int cipher_id, const uint8_t *key, cons
                 st = rc;
                 break;
             }
+            /* a relaunch by group_launch starts this slot's context history
+               afresh, and the new workgroup serves k and caches h_ctx: note it
+               again, or freeing the state would not park this group and the
+               round keys would stay in its LDS */
+            if (h_ctx) worker_note_ctx(w, h_ctx);
         }
         if (host_ns() - h2 > WAIT_LIMIT_NS) { /* no answer: drained, then reused */
             worker_abandon(w, k);

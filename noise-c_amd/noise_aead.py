@@ -82,7 +82,8 @@ class NoiseAeadRagged(C.Structure):
 
 FLAG_FAST = 1
 FLAG_CT_GHASH = 2
-FLAG_VERIFY_FIRST = 4
+FLAG_VERIFY_FIRST = 4  # the default open order since round 6 (accepted, overrides ONE_PASS)
+FLAG_ONE_PASS = 8      # opt-in: ChaChaPoly FAST opens decrypt while authenticating
 _LIB = None
 
 

@@ -15,6 +15,8 @@ an N-GPU run, so each rank checks its own shard:
       mixed_layout), ranks 0..7, sealed through the reference build (its AES
       is ~30x faster than the bit-serial oracle); every 128th record
       re-sealed by the oracle as a cross-check.
+  c5s: the same layout rule at 16 Ki records / 64 states per rank (the GPU
+      tests' multi-rank rehearsal), ranks 0..7 (`--c5s` adds it alone).
 
 Each digest is SHA-256 over the sealed records (ct || tag) in record order,
 stride padding excluded.  Rank 0 / W = 1 entries equal config_digests.json's.
@@ -87,11 +89,11 @@ def c4_slices():
     return {str(W): [h.hexdigest() for h in v] for W, v in hs.items()}
 
 
-def c5_rank(r):
+def c5_rank(r, name="c5"):
     from bench import CONFIGS as BC, mixed_layout
     o = Oracle()
     ref = RefLib()
-    R, S = BC["c5"]["records"], BC["c5"]["states"]
+    R, S = BC[name]["records"], BC[name]["states"]
     lay = mixed_layout(R, S, r)
     pt = o.fill(SEED_PT, lay["total"], r << 40)
     keys = {}
@@ -110,7 +112,26 @@ def c5_rank(r):
     return r, h.hexdigest()
 
 
+def c5s_rank(r):
+    return c5_rank(r, "c5s")
+
+
+def add_c5s():
+    """`--c5s`: add the reduced C5 rehearsal layout's rank digests (bench.py
+    CONFIGS["c5s"]: 16 Ki records / 64 states per rank) to the existing file."""
+    path = os.path.join(ROOT, "tests", "golden", "shard_digests.json")
+    with open(path) as f:
+        out = json.load(f)
+    with Pool(8) as p:
+        res = p.map(c5s_rank, range(RANKS))
+    out["configs"]["c5s"] = {"rank_sealed_sha256": [d for _, d in sorted(res)]}
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
+    if sys.argv[1:2] == ["--c5s"]:
+        return add_c5s()
     t = time.time()
     jobs = []
     for name, cipher, L, ad, ins, outs in (("c2", CHACHA, 1400, 0, 1408, 1536),
@@ -125,6 +146,8 @@ def main():
     for name, r, d in res:
         out["configs"][name].setdefault("rank_sealed_sha256", [None] * RANKS)[r] = d
     out["configs"]["c5"] = {"rank_sealed_sha256": [d for _, d in sorted(c5)]}
+    with Pool(8) as p:
+        out["configs"]["c5s"] = {"rank_sealed_sha256": [d for _, d in sorted(p.map(c5s_rank, range(RANKS)))]}
     print("weak + c5", f"{time.time() - t:.0f}s")
     t = time.time()
     out["configs"]["c4"] = {"world_rank_sealed_sha256": c4_slices()}

@@ -112,7 +112,7 @@ def test_gpus_must_match_world_size():
 
 def test_shard_goldens_cover_every_rank():
     """bench.py verifies each rank's sealed shard against these digests."""
-    for cfg in ("c2", "c3", "perf", "c5"):
+    for cfg in ("c2", "c3", "perf", "c5", "c5s"):
         for r in range(8):
             assert bench.shard_golden(cfg, r, 8, False), (cfg, r)
     for w in (1, 2, 4, 8):

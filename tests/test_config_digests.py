@@ -3,8 +3,9 @@
 tests/golden/config_digests.json holds, for C2, C3 and C4 at N = 1, the
 SHA-256 of the packed plaintexts and of the packed sealed records (ct || tag)
 that the CPU oracle produces over bench.py's synthetic inputs (SplitMix64,
-SURVEY.md §8d); the C2 digest was also reproduced through the reference's own
-CipherState API (`reference_checked`).  The GPU test regenerates the same
+SURVEY.md §8d); every one of them (C2, C3, C4, C5, perf) was also
+reproduced through the reference's own CipherState API, one call per record
+(`reference_checked`; gen_config_digests.py --ref-check).  The GPU test regenerates the same
 inputs in HBM, seals every record of the full batch with the gfx950 kernels,
 and compares the digest of every output byte; the open then has to accept
 every record and give back the plaintext digest.
@@ -36,6 +37,14 @@ def test_oracle_reproduces_c2_digest(oracle):
     oracle.seal_uniform(c["cipher"], keys, np.zeros(1, dtype=np.uint64), N, pt, ins, ct, outs, L, N)
     assert hashlib.sha256(ct.reshape(N, outs)[:, :L + 16].tobytes()).hexdigest() == c["sealed_sha256"]
     assert c.get("reference_checked")
+
+
+def test_every_config_digest_reference_checked():
+    """no full-size golden digest rests on the oracle
+    alone — C3 (AES-GCM) and C4 (4096 states) were re-derived through the
+    reference build too."""
+    for name, c in _golden().items():
+        assert c.get("reference_checked") is True, name
 
 
 @pytest.mark.gpu
@@ -164,7 +173,7 @@ def test_c5_shard_digest_on_gpu(rank):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,lanes,vf", [("c2", 0, False), ("c2", 4, False), ("c3", 0, False),
                                            ("c2", 0, True), ("c3", 0, True), ("c4", 0, False),
-                                           ("perf", 0, False)])
+                                           ("c4", 0, True), ("perf", 0, True)])
 def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     """The kernels bench.py times: C2 / C3 at full size
     through noise_aead_dev_duplex_uniform at the bench's 128-B record slots
@@ -175,8 +184,10 @@ def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     :107-133 / cipher-aesgcm.c:156-170 bytes); the open half, over a batch
     sealed beforehand with 64 records tampered, accepts every other record
     with the plaintext digest and rejects (zeroes) exactly the tampered ones.
-    vf: the open half with NOISE_AEAD_FLAG_VERIFY_FIRST (the bench's
-    --verify-first line, still one launch): rejected records never written.
+    vf: the open half in the default order — verify first since round 6,
+    the bench's default line, still one launch: rejected records never
+    written; not vf: the open half with NOISE_AEAD_FLAG_ONE_PASS (the bench's
+    --one-pass line): rejected records zeroed.
     c4: the timed kernel of C4 — the one-lane duplex
     over 4096 states x 256 records; perf: the duplex of 1024-B records with
     32 B of AD each (both reference-checked digests, the perf one through
@@ -227,7 +238,7 @@ def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     st = torch.full((N,), 9, dtype=torch.uint8, device="cuda")
     sj = A.uniform_job(inp=pt.data_ptr(), out=ct_a.data_ptr(), in_stride=ins, out_stride=outs, **common)
     oj = A.uniform_job(inp=ct_b.data_ptr(), out=back.data_ptr(), in_stride=outs, out_stride=ins,
-                       status=st.data_ptr(), flags=4 if vf else 0, **common)
+                       status=st.data_ptr(), flags=0 if vf else A.FLAG_ONE_PASS, **common)
     assert A.dev_duplex(cipher, sj, oj, sp) == 0
     torch.cuda.synchronize()
     sealed = ct_a.view(N, outs)[:, :L + 16].contiguous().cpu().numpy()
@@ -241,8 +252,8 @@ def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     good = torch.ones(N, dtype=torch.bool, device="cuda")
     good[torch.from_numpy(bad).to("cuda")] = False
     assert torch.equal(bv[good], pv[good])
-    # rejected records: zeroed out of place (one-pass ChaChaPoly) / never
-    # written (verify-first, and every AES-GCM open)
+    # rejected records: zeroed out of place (ONE_PASS ChaChaPoly) / never
+    # written (verify-first: the default, and every AES-GCM open)
     fill = 0xA5 if (vf or cipher == A.AESGCM) else 0
     assert int(bv[~good].max().item()) == fill
     assert int(bv[~good].min().item()) == fill

@@ -39,6 +39,11 @@ def sync():
     _torch().cuda.synchronize()
 
 
+# NOISE_AEAD_FLAG_*: verify-first is the default open order (round 6);
+# ONE_PASS opts a ChaChaPoly FAST open into decrypt-while-authenticating
+FLAG_CT_GHASH, FLAG_VERIFY_FIRST, FLAG_ONE_PASS = 2, 4, 8
+
+
 def prepare(aead, cipher, keys):
     torch = _torch()
     keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 32)
@@ -74,10 +79,11 @@ def gpu_uniform(aead, open_, cipher, keys, nonce_base, rps, inp, in_stride, leng
 
 def rejected_fill(cipher, out_init, flags=0):
     """What a rejected record's output holds after an out-of-place open:
-    untouched (its prior fill) when the open verified first — every AES-GCM
-    open (aead_api.hip open_vf) and NOISE_AEAD_FLAG_VERIFY_FIRST ones — and
-    zeroed after a one-pass ChaChaPoly open."""
-    return out_init if (cipher == AES or flags & 4) else 0
+    untouched (its prior fill) when the open verified first — every open by
+    default since round 6 (aead_api.hip open_vf; every AES-GCM open always)
+    — and zeroed after a ChaChaPoly open that opted into
+    NOISE_AEAD_FLAG_ONE_PASS (VERIFY_FIRST overrides it)."""
+    return 0 if (cipher == CHACHA and flags & FLAG_ONE_PASS and not flags & FLAG_VERIFY_FIRST) else out_init
 
 
 def oracle_seal_records(oracle, cipher, keys, nonce_base, rps, pt, in_stride, length, count,
@@ -123,8 +129,11 @@ LENS = [0, 1, 15, 16, 17, 48, 56, 63, 64, 65, 127, 128, 129, 191, 192, 255, 256,
 @pytest.mark.parametrize("rps", [13, 16])
 def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed, rps):
     """rps=13: states straddle waves; rps=16: every 4/8-lane wave holds one
-    state (the wave-uniform-key kernels), the last wave partial."""
+    state (the wave-uniform-key kernels), the last wave partial.  The rps=13
+    opens opt into NOISE_AEAD_FLAG_ONE_PASS, the rps=16 ones take the default
+    (verify-first) order."""
     rng = np.random.default_rng(1000 + lanes + 7 * packed + (cipher & 3) + rps)
+    oflags = FLAG_ONE_PASS if rps == 13 else 0
     for L in LENS:
         count = 37 if rps == 13 else 70  # the last state partial
         S = (count + rps - 1) // rps
@@ -144,24 +153,26 @@ def test_uniform_seal_open_vs_oracle(aead, gpu, oracle, cipher, lanes, packed, r
             pos = b * out_stride + int(rng.integers(0, L + 16))
             ct[pos] ^= 1 << int(rng.integers(0, 8))
         back, st = gpu_uniform(aead, True, cipher, keys, nb, rps, ct, out_stride, L, count,
-                               in_stride, lanes=lanes, out_init=0x5A)
+                               in_stride, lanes=lanes, out_init=0x5A, flags=oflags)
         for i in range(count):
             seg = back[i * in_stride: i * in_stride + L]
             if i in bad:
                 assert st[i] == 1, f"tamper not detected len={L} rec={i}"
-                assert np.all(seg == rejected_fill(cipher, 0x5A)), "rejected record's output"
+                assert np.all(seg == rejected_fill(cipher, 0x5A, oflags)), "rejected record's output"
             else:
                 assert st[i] == 0, f"valid record rejected len={L} rec={i}"
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L])
 
 
 @pytest.mark.parametrize("cipher,lanes", [(CHACHA, 0), (CHACHA, 1), (CHACHA, 4), (AES, 0)])
-def test_uniform_staged_kernels(aead, gpu, oracle, cipher, lanes):
+@pytest.mark.parametrize("oflags", [0, FLAG_ONE_PASS])
+def test_uniform_staged_kernels(aead, gpu, oracle, cipher, lanes, oflags):
     """FAST layouts with one state per 256 records: the LDS-staged kernels
     (ChaChaPoly wave-uniform key at one and four lanes per record, AESGCM
     replicated T-tables) on a batch whose last workgroup is partial, every
-    record vs the oracle, with AD."""
-    rng = np.random.default_rng(4242 + (cipher & 3) + 100 * lanes)
+    record vs the oracle, with AD; opens in the default (verify-first) order
+    and with NOISE_AEAD_FLAG_ONE_PASS."""
+    rng = np.random.default_rng(4242 + (cipher & 3) + 100 * lanes + oflags)
     rps, count = 256, 600
     S = (count + rps - 1) // rps
     for L, adl in [(0, 0), (1, 0), (15, 0), (16, 0), (17, 0), (100, 0), (1400, 0), (1401, 0),
@@ -183,11 +194,11 @@ def test_uniform_staged_kernels(aead, gpu, oracle, cipher, lanes):
         for b in bad:
             ct[b * out_stride + int(rng.integers(0, L + 16))] ^= 0x80
         back, st = gpu_uniform(aead, True, cipher, keys, nb, rps, ct, out_stride, L, count,
-                               in_stride, out_init=0x3C, lanes=lanes, **kw)
+                               in_stride, out_init=0x3C, lanes=lanes, flags=oflags, **kw)
         for i in range(count):
             seg = back[i * in_stride: i * in_stride + L]
             if i in bad:
-                assert st[i] == 1 and np.all(seg == rejected_fill(cipher, 0x3C)), f"len={L} rec={i}"
+                assert st[i] == 1 and np.all(seg == rejected_fill(cipher, 0x3C, oflags)), f"len={L} rec={i}"
             else:
                 assert st[i] == 0, f"len={L} rec={i}"
                 assert np.array_equal(seg, pt[i * in_stride: i * in_stride + L]), f"len={L} rec={i}"
@@ -199,14 +210,16 @@ def test_uniform_staged_kernels(aead, gpu, oracle, cipher, lanes):
                                                   (CHACHA, 1, 64, 21), (AES, 0, 256, 0),
                                                   (AES, 0, 13, 0), (CHACHA, 4, 256, 21),
                                                   (AES, 0, 256, 21)])
-def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes, rps, adl):
+@pytest.mark.parametrize("oflags", [0, FLAG_ONE_PASS])
+def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes, rps, adl, oflags):
     """Open in place (in == out, one stride): every verified record becomes
     its plaintext and every rejected one reads exactly as given — CT and tag
-    bytes — including in the single-pass staged kernels (ChaChaPoly and
-    AES-GCM), which write plaintext before the verdict and re-encrypt on
-    failure; with and without associated data."""
+    bytes — in the default (verify-first) order and in the single-pass
+    ChaChaPoly kernels (NOISE_AEAD_FLAG_ONE_PASS), which write plaintext
+    before the verdict and re-encrypt on failure; with and without associated
+    data."""
     torch = _torch()
-    rng = np.random.default_rng(808 + lanes + rps + (cipher & 3) + adl)
+    rng = np.random.default_rng(808 + lanes + rps + (cipher & 3) + adl + oflags)
     for L, count in [(1400, 700), (0, 70), (17, 300), (4096, 40), (100, 257)]:
         S = (count + rps - 1) // rps
         keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
@@ -229,7 +242,7 @@ def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes
                                 out_stride=stride_, length=L, n_records=count, recs_per_state=rps,
                                 status=d_st.data_ptr(), lanes=lanes, stream=stream(),
                                 ad=d_ad.data_ptr() if adl else 0, ad_stride=32 if adl else 0,
-                                ad_len=adl) == 0
+                                ad_len=adl, flags=oflags) == 0
         sync()
         back, st = d_buf.cpu().numpy(), d_st.cpu().numpy()
         for i in range(count):
@@ -240,7 +253,6 @@ def test_open_in_place_rejects_leave_ciphertext(aead, gpu, oracle, cipher, lanes
                 assert st[i] == 0 and np.array_equal(back[o:o + L], pt[o:o + L]), (L, i)
 
 
-FLAG_CT_GHASH, FLAG_VERIFY_FIRST = 2, 4
 DUPLEX_CASES = [((1400, 700, 350), (1400, 300, 100)), ((100, 64, 16), (1401, 513, 513)),
                 ((0, 33, 16), (65, 1000, 16)), ((4096, 5, 5), (17, 0, 1))]
 # one state per 256 records (the AES duplex kernel, the bench's wave-uniform
@@ -250,23 +262,25 @@ SLOT_CASES = [((1400, 1024, 512), (1400, 768, 256)), ((1400, 512, 256), (1024, 2
 
 
 @pytest.mark.parametrize("cipher,lanes,layout,flags", [
-    (CHACHA, 4, "fast", 0), (CHACHA, 8, "fast", 0), (CHACHA, 4, "packed", 0), (AES, 0, "fast", 0),
-    (CHACHA, 1, "fast", 0), (CHACHA, 1, "slot128", 0), (CHACHA, 0, "slot128", 0),
-    (CHACHA, 4, "slot128", 0), (CHACHA, 8, "slot128", 0), (AES, 0, "slot128", 0),
+    (CHACHA, 4, "fast", FLAG_ONE_PASS), (CHACHA, 8, "fast", FLAG_ONE_PASS), (CHACHA, 4, "packed", 0),
+    (AES, 0, "fast", 0), (CHACHA, 1, "fast", FLAG_ONE_PASS), (CHACHA, 1, "slot128", FLAG_ONE_PASS),
+    (CHACHA, 0, "slot128", FLAG_ONE_PASS), (CHACHA, 4, "slot128", FLAG_ONE_PASS),
+    (CHACHA, 8, "slot128", FLAG_ONE_PASS), (AES, 0, "slot128", 0),
     (AES, 0, "slot128", FLAG_CT_GHASH), (CHACHA, 4, "slot128", FLAG_VERIFY_FIRST),
     (AES, 0, "slot128", FLAG_VERIFY_FIRST), (CHACHA, 1, "slot128", FLAG_VERIFY_FIRST),
-    (CHACHA, 1, "fast", FLAG_VERIFY_FIRST)])
+    (CHACHA, 1, "fast", 0), (CHACHA, 0, "slot128", 0), (CHACHA, 4, "slot128", 0),
+    (CHACHA, 1, "slot128", FLAG_ONE_PASS | FLAG_VERIFY_FIRST)])
 def test_duplex_vs_oracle(aead, gpu, oracle, cipher, lanes, layout, flags):
     """noise_aead_dev_duplex_uniform: seal job A and open job B (other keys,
     nonces, length, record count; some records tampered) in one call must
     equal the two separate calls — i.e. the oracle — byte for byte.  ChaCha
     FAST layouts run the one-launch chachapoly_duplex_staged kernel; AES-GCM
     with one state per 256 records runs gcm_duplex_fused (plain and CT
-    GHASH); a VERIFY_FIRST open shares the launch with the one-lane ChaCha
-    kernel (AUTH + DEC passes) and the AES duplex kernels, the others run two
-    launches.  A rejected
-    record's output is zeroed (one-pass opens) or never written
-    (VERIFY_FIRST)."""
+    GHASH); a verify-first open (the default; VERIFY_FIRST also overrides
+    ONE_PASS) shares the launch with the one-lane ChaCha kernel (AUTH + DEC
+    passes) and the AES duplex kernels, the others run two launches.  A
+    rejected record's output is zeroed (NOISE_AEAD_FLAG_ONE_PASS opens) or
+    never written (verify-first)."""
     torch = _torch()
     rng = np.random.default_rng(3131 + lanes + (cipher & 3) + len(layout) + flags)
     for (La, na, rpsa), (Lb, nb_, rpsb) in (SLOT_CASES if layout == "slot128" else DUPLEX_CASES):
@@ -888,7 +902,7 @@ def test_interleaved_slots_one_buffer(aead, gpu, oracle, cipher):
         assert np.array_equal(back[o:o + L], pt[o:o + L]), i
 
 
-@pytest.mark.parametrize("flags", [0, FLAG_VERIFY_FIRST])
+@pytest.mark.parametrize("flags", [FLAG_ONE_PASS, 0])
 def test_duplex_solo_runs(aead, gpu, oracle, flags):
     """chachapoly_duplex_solo places the paired blocks in runs of the CU count
     (seal run, open run, ...) and the remainder block by block: job sizes

@@ -8,7 +8,8 @@ Every output byte is compared with the CPU oracle (oracle/noise_oracle.c,
 pinned to the reference by tests/test_oracle.py): ciphertext and tag of every
 record, the accept/reject decision of every open, the plaintext of accepted
 records, and the bytes of rejected ones (in place: as given; out of place:
-zeroed by a one-pass open, never written by a verify-first one).
+zeroed by a NOISE_AEAD_FLAG_ONE_PASS open, never written by a verify-first
+one — the default order).
 """
 import numpy as np
 import pytest
@@ -54,15 +55,17 @@ def _ragged_batch(rng, count, S):
 
 
 @pytest.mark.parametrize("vf", [False, True])
-@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("inplace", [False, True, "mixed"])
 def test_ragged_seg_vs_oracle(aead, gpu, oracle, vf, inplace):
     """20 000 records (past the segmented kernel's 16 384-record threshold):
     0 B - 64 KiB, the edge lengths of every segment count K = 1..16, two
     refused lengths (status 2, nothing written), AD on a tenth, 300 states,
-    descriptors shuffled; seal out of place, then open (in place or out of
-    place, one-pass or verify-first) with every 41st record tampered."""
+    descriptors shuffled; seal out of place, then open (in place, out of
+    place, or mixed — every other record's output in place, the rest in a
+    second region of the same buffer, ADVICE r5 — one-pass or verify-first)
+    with every 41st record tampered."""
     torch = __import__("torch")
-    rng = np.random.default_rng(5150 + 2 * vf + inplace)
+    rng = np.random.default_rng(5150 + 2 * vf + (2 if inplace == "mixed" else int(inplace)))
     count, S = 20000, 300
     keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
     ctx, _k = prepare(aead, CHACHA, keys)
@@ -92,11 +95,25 @@ def test_ragged_seg_vs_oracle(aead, gpu, oracle, vf, inplace):
     badm = (np.arange(count) % 41 == 7) & ~refused
     for i in np.nonzero(badm)[0]:
         tampered[offs[i] + int(rng.integers(0, lens[i] + 16))] ^= 0x08
-    d_in = dev(tampered)
-    d_out = d_in if inplace else torch.full((total,), 0x5A, dtype=torch.uint8, device="cuda")
+    if inplace == "mixed":
+        # one buffer: the ciphertext at [0, total), out-of-place outputs at
+        # [total, 2 total); record i is in place when i is even
+        ip = np.arange(count) % 2 == 0
+        buf = np.concatenate([tampered, np.full(total, 0x5A, dtype=np.uint8)])
+        d_in = d_out = dev(buf)
+        orecs = recs.copy()
+        orecs["out_off"] = np.where(ip, offs, offs + total).astype(np.uint64)
+        d_orecs = dev(orecs.view(np.uint8))
+        oo = np.where(ip, offs, offs + total)
+    else:
+        ip = np.full(count, bool(inplace))
+        d_in = dev(tampered)
+        d_out = d_in if inplace else torch.full((total,), 0x5A, dtype=torch.uint8, device="cuda")
+        d_orecs = d_recs
+        oo = offs
     d_st.fill_(9)
-    flags = aead.FLAG_FAST | (aead.FLAG_VERIFY_FIRST if vf else 0)
-    assert aead.dev_ragged(True, CHACHA, ctx_base=ctx.data_ptr(), recs=d_recs.data_ptr(),
+    flags = aead.FLAG_FAST | (0 if vf else aead.FLAG_ONE_PASS)  # vf: the default order
+    assert aead.dev_ragged(True, CHACHA, ctx_base=ctx.data_ptr(), recs=d_orecs.data_ptr(),
                            inp=d_in.data_ptr(), out=d_out.data_ptr(), n_records=count,
                            ad=d_ad.data_ptr(), status=d_st.data_ptr(), flags=flags,
                            stream=stream()) == 0
@@ -106,17 +123,17 @@ def test_ragged_seg_vs_oracle(aead, gpu, oracle, vf, inplace):
     assert np.array_equal(st, want), np.nonzero(st != want)[0][:8]
     back = d_out.cpu().numpy()
     for i in range(count):
-        o, L = int(offs[i]), int(lens[i])
+        o, L, q = int(offs[i]), int(lens[i]), int(oo[i])
         if refused[i]:
-            seg = back[o:o + 16]
-            assert np.array_equal(seg, tampered[o:o + 16] if inplace else np.full(16, 0x5A, np.uint8)), i
+            seg = back[q:q + 16]
+            assert np.array_equal(seg, tampered[o:o + 16] if ip[i] else np.full(16, 0x5A, np.uint8)), i
         elif badm[i]:
-            if inplace:
-                assert np.array_equal(back[o:o + L + 16], tampered[o:o + L + 16]), i
+            if ip[i]:
+                assert np.array_equal(back[q:q + L + 16], tampered[o:o + L + 16]), (i, L)
             else:
-                assert np.all(back[o:o + L] == (0x5A if vf else 0)), i
+                assert np.all(back[q:q + L] == (0x5A if vf else 0)), (i, L)
         else:
-            assert np.array_equal(back[o:o + L], pt[o:o + L]), (i, L)
+            assert np.array_equal(back[q:q + L], pt[o:o + L]), (i, L)
 
 
 LENS2 = [0, 1, 15, 16, 63, 64, 65, 127, 128, 191, 192, 1023, 1400, 1401, 4096, 5000, 65519]
@@ -146,7 +163,7 @@ def test_uniform_seg2_vs_oracle(aead, gpu, oracle, vf, rps):
         bad = sorted(set(rng.integers(0, count, 4).tolist()))
         for b in bad:
             ct[b * outs + int(rng.integers(0, L + 16))] ^= 0x20
-        flags = aead.FLAG_VERIFY_FIRST if vf else 0
+        flags = aead.FLAG_VERIFY_FIRST if vf else aead.FLAG_ONE_PASS
         back, st = gpu_uniform(aead, True, CHACHA, keys, nb, rps, ct, outs, L, count, ins, lanes=2,
                                out_init=0x5A, flags=flags)
         for i in range(count):

@@ -1,10 +1,13 @@
-"""NOISE_AEAD_FLAG_VERIFY_FIRST: the strict open order.
+"""The verify-first open order (the default of every open
+since round 6; NOISE_AEAD_FLAG_VERIFY_FIRST requests it
+explicitly).
 
 The reference's ref backends authenticate first and decrypt only a record
 whose tag verified (src/backend/ref/cipher-chachapoly.c:135-141,
-cipher-aesgcm.c:172-188).  The default FAST-layout opens of this library run
-in one pass and undo a rejected record's plaintext before the kernel ends;
-with VERIFY_FIRST no byte of a rejected record's output is ever written —
+cipher-aesgcm.c:172-188).  The opt-in NOISE_AEAD_FLAG_ONE_PASS FAST-layout
+ChaChaPoly opens run in one pass and undo a rejected record's plaintext
+before the kernel ends; in the default order (no flag) and with
+VERIFY_FIRST no byte of a rejected record's output is ever written —
 not plaintext, not zeros.  So out of place a rejected record's output still
 holds its sentinel fill, and in place its CT || tag reads back as given; every
 verified record equals the oracle's plaintext.  Uniform (staged and generic
@@ -26,9 +29,11 @@ REC_DT = [("in_off", "<u8"), ("out_off", "<u8"), ("nonce", "<u8"), ("ctx_off", "
                                               (CHACHA, 1, 16), (CHACHA, 1, 64), (CHACHA, 64, 16), (AES, 0, 256),
                                               (AES, 0, 13)])
 @pytest.mark.parametrize("in_place", [False, True])
-def test_uniform_verify_first(aead, gpu, oracle, cipher, lanes, rps, in_place):
+@pytest.mark.parametrize("vflag", [VF, 0])
+def test_uniform_verify_first(aead, gpu, oracle, cipher, lanes, rps, in_place, vflag):
+    """vflag 0: no flag at all — the default open order must be the strict one."""
     import torch
-    rng = np.random.default_rng(31 + lanes + rps + (cipher & 3) + 100 * in_place)
+    rng = np.random.default_rng(31 + lanes + rps + (cipher & 3) + 100 * in_place + vflag)
     for L, count, adl in [(1400, 600, 0), (0, 40, 0), (17, 300, 0), (4096, 30, 0), (1400, 257, 24)]:
         S = (count + rps - 1) // rps
         keys = rng.integers(0, 256, (S, 32), dtype=np.uint8)
@@ -54,7 +59,7 @@ def test_uniform_verify_first(aead, gpu, oracle, cipher, lanes, rps, in_place):
         assert aead.dev_uniform(True, cipher, ctx=ctx.data_ptr(), nonce_base=d_nb.data_ptr(),
                                 inp=d_ct.data_ptr(), out=d_out.data_ptr(), in_stride=stride_ct,
                                 out_stride=out_stride, length=L, n_records=count, recs_per_state=rps,
-                                status=d_st.data_ptr(), lanes=lanes, flags=VF, stream=stream(),
+                                status=d_st.data_ptr(), lanes=lanes, flags=vflag, stream=stream(),
                                 ad=d_ad.data_ptr() if adl else 0, ad_stride=32 if adl else 0,
                                 ad_len=adl) == 0
         sync()

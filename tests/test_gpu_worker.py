@@ -234,3 +234,18 @@ def test_group_stays_while_one_slot_is_busy(gpu):
                         "--group-idle"], env=dict(os.environ, **env), timeout=110, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "group_idle_ok 1" in r.stdout
+
+
+def test_relaunch_mid_wait_keeps_context_history(gpu):
+    """a call whose group leaves after the call found it up and
+    before its request was served relaunches the group from its wait loop;
+    the relaunch starts the slot's context history afresh, so the call notes
+    its AES-GCM context again.  Freeing the state then parks the relaunched
+    group (NOISE_AEAD_DEBUG_WORKER_LEAVE=1 forces the race on every call;
+    tests/worker_mode_check.py --relaunch-free)."""
+    env = {"NOISE_AEAD_DEBUG_WORKER_IDLE_MS": "10000", "NOISE_AEAD_DEBUG_WORKER_LEAVE": "1"}
+    r = subprocess.run([sys.executable, "-u", os.path.join(os.path.dirname(__file__), "worker_mode_check.py"),
+                        "--relaunch-free"], env=dict(os.environ, **env), timeout=110, capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "relaunch_free_ok 1" in r.stdout

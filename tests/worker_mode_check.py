@@ -155,6 +155,40 @@ def free_concurrent():
     return 0 if ok else 1
 
 
+def relaunch_free():
+    """--relaunch-free (run with NOISE_AEAD_DEBUG_WORKER_LEAVE=1 and
+    NOISE_AEAD_DEBUG_WORKER_IDLE_MS=10000): every single call's group leaves
+    after the call checked it was up and before the request is posted, so the
+    call's wait loop relaunches the group and the new workgroup serves the
+    request and caches the AES-GCM context.  Freeing the state must still park
+    that group within 200 ms (the relaunch used to wipe the slot's
+    context history).  The call's result is checked against the oracle.
+    Prints "relaunch_free_ok 1"."""
+    import time
+    lib = aead.lib()
+    lib.noise_aead_debug_workers_resident.restype = int
+    orc = O.Oracle()
+    key = bytes(range(7, 39))
+    _, st = aead.CipherState.new_by_id(0x4302)
+    assert st.init_key(key) == 0
+    pt = bytes(range(200))
+    ct = st.seal(pt)
+    if ct != orc.encrypt(0x4302, key, 0, pt):
+        print("seal mismatch")
+        return 1
+    time.sleep(0.05)
+    res0 = lib.noise_aead_debug_workers_resident()
+    t0 = time.time()
+    st.free()
+    while lib.noise_aead_debug_workers_resident() and time.time() - t0 < 0.2:
+        time.sleep(0.001)
+    res1 = lib.noise_aead_debug_workers_resident()
+    ok = res0 >= 1 and res1 == 0
+    print("resident", res0, res1)
+    print("relaunch_free_ok", 1 if ok else 0)
+    return 0 if ok else 1
+
+
 def group_idle():
     """--group-idle (run with NOISE_AEAD_WORKER_QUEUES=1,
     NOISE_AEAD_WORKER_SLOTS=2, NOISE_AEAD_DEBUG_WORKER_IDLE_MS=20): one
@@ -211,4 +245,6 @@ if __name__ == "__main__":
         sys.exit(free_check())
     if "--free-concurrent" in sys.argv:
         sys.exit(free_concurrent())
+    if "--relaunch-free" in sys.argv:
+        sys.exit(relaunch_free())
     sys.exit(main())

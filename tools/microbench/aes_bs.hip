@@ -19,6 +19,7 @@
 // SIMD-cycles per block (at the in-kernel clock) for each.
 // build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../../include -I../../noise-c_amd/csrc aes_bs.hip -o aes_bs
 #include "../../noise-c_amd/csrc/aesgcm.hip"
+#include "aes_bs.h" /* the bitsliced circuit (the round-4 A/B kernels' shared code) */
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -95,7 +96,7 @@ static void h_encrypt(const uint8_t rk[15][16], uint8_t s[16])
 /* ------------------------------------------------------------ bitsliced */
 struct BsKey { uint32_t m[15][128]; };
 
-/* bs_sbox, bs_x3, bs2_round, bs_partner, bs_transpose32: noise-c_amd/csrc/aes_bs.h
+/* bs_sbox, bs_x3, bs2_round, bs_partner, bs_transpose32: tools/microbench/aes_bs.h
    (included through aesgcm.hip) */
 
 #define BS_SBOX(q, b) bs_sbox(q[8 * (b)], q[8 * (b) + 1], q[8 * (b) + 2], q[8 * (b) + 3], q[8 * (b) + 4], \
