@@ -377,7 +377,12 @@ NA_DEV void poly_tree_close(Fe acc, int k, const Fe &r, const Mul &mr, uint32_t 
    computing a block no one reads.  The issue slots are the same; what it
    saves is energy, and the chip holds its clock by energy under this load
    (MI355X_MICROARCH.md, DVFS give-back): C4 +1.1 %, perf +0.9 % in three
-   interleaved rounds (profiles/r02/mask_idle_ab.jsonl). */
+   interleaved rounds (profiles/r02/mask_idle_ab.jsonl).  RUNS (the staged
+   kernels: four waves per SIMD) issues the block in runs with priority
+   toggles (aead_device.h chacha20_block_runs, round 6); the windowed
+   kernels, whose small batches often hold under one wave per SIMD, keep
+   hipcc's schedule. */
+template <bool RUNS = false>
 NA_DEV void slot_block(const uint32_t key[8], const ChaPre &pre, int v, uint32_t n_lo,
                        uint32_t n_hi, uint32_t x[16])
 {
@@ -386,7 +391,8 @@ NA_DEV void slot_block(const uint32_t key[8], const ChaPre &pre, int v, uint32_t
         for (int i = 0; i < 16; ++i) x[i] = 0;
         return;
     }
-    chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+    if constexpr (RUNS) chacha20_block_runs<2, 0, 0>(key, pre, (uint32_t)v, n_lo, n_hi, x);
+    else chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
 }
 
 template <int K, bool FAST>
@@ -875,7 +881,7 @@ NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
         /* next step's bytes go into the other tile while this one computes */
         if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
-        slot_block(key, pre, v, n_lo, n_hi, x);
+        slot_block<true>(key, pre, v, n_lo, n_hi, x);
         if (m == 0) {
             Fe r;
             poly_key_bcast(x, gbase + (int)g.o, r, s);
@@ -955,7 +961,7 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
         __builtin_amdgcn_wave_barrier();
         if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
-        slot_block(key, pre, v, n_lo, n_hi, x);
+        slot_block<true>(key, pre, v, n_lo, n_hi, x);
         if (m == 0) {
             Fe r;
             poly_key_bcast(x, gbase + (int)g.o, r, s);
@@ -1190,34 +1196,37 @@ NA_DEV SoloRec solo_rec(const UniformArgs &a, uint32_t wave_job)
    (hipcc waits before an LDS read for the youngest LDS-DMA; reading the tile
    after issuing the next DMA, as the 4-lane kernels do, made every step wait
    for the DMA it had just issued and serialised the stores behind it.) */
-/* The key stream of a one-lane step (blocks c0, c0 + 1 of the lane's
-   record).  NA_CHACHA_RUNS (round-6 A/B): 0 = chacha20_block_pre per block
-   (hipcc's schedule); 1 = the two blocks in lock step issued in runs
-   (chacha20_2block_runs) without priority toggles; 2 = rotate runs at
-   s_setprio 2, fast runs at 0; 3 = 3 / 1. */
-#ifndef NA_CHACHA_RUNS
-#define NA_CHACHA_RUNS 0
-#endif
-#if NA_CHACHA_RUNS
+/* The key stream of a one-lane step: blocks c0 and c0 + 1 of the lane's
+   record in lock step, issued in runs, rotate runs at s_setprio 2 and fast
+   runs at 0 (aead_device.h chacha20_2block_runs; round 6).  Measured
+   against hipcc's schedule of two chacha20_block_pre calls, interleaved on
+   one box (profiles/r06/runs_ab/): C2 duplex +4 %, C4 +10 %, perf +8 %,
+   C5 +5 %; toggles 3 / 1 measured the same, runs without the toggles
+   nothing.  A standalone one-lane launch of < 2 waves per SIMD lost 11 %
+   with it (a lone wave has no partner to fill the slots a rotate run
+   leaves), so those keep hipcc's schedule (RUNS = false). */
+template <bool RUNS>
 NA_DEV void solo_blocks2(const uint32_t key[8], const ChaPre &pre, uint32_t c0, uint32_t n_lo, uint32_t n_hi,
-                         uint32_t (&x0)[16], uint32_t (&x1)[16])
+                         uint32_t (&x0)[16], uint32_t (&x1)[16], bool early = false)
 {
-#if NA_CHACHA_RUNS == 1
-    chacha20_2block_runs<-1, -1, -1>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
-#elif NA_CHACHA_RUNS == 2
-    chacha20_2block_runs<2, 0, 0>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
-#else
-    chacha20_2block_runs<3, 1, 1>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
+    if constexpr (RUNS) {
+#ifdef NA_RUNS_PROGRESS /* A/B: a wave in the first half of its steps one level up */
+        if (early) chacha20_2block_runs<3, 1, 1>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
+        else
 #endif
+        chacha20_2block_runs<2, 0, 0>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
+    } else {
+        chacha20_block_pre(key, pre, c0, n_lo, n_hi, x0);
+        chacha20_block_pre(key, pre, c0 + 1, n_lo, n_hi, x1);
+    }
 }
-#endif
 
 /* solo_pass modes: SEAL and OPEN1 (the opt-in one-pass open,
    NOISE_AEAD_FLAG_ONE_PASS) as above; the verify-first open (the default)
    runs solo_auth and then solo_dec_rev (below). */
 enum SoloMode { SOLO_SEAL, SOLO_OPEN1 };
 
-template <int MODE>
+template <int MODE, bool RUNS>
 NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const uint32_t key[8],
                       const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, const R32 &r, P32 &h)
 {
@@ -1237,21 +1246,19 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
            ahead lowers its priority (aead_device.h): C2 +5-8 %, C4 +0.5 %
            (profiles/r04/solo_prio_ab.jsonl). */
         prio_by_progress(m, q.S);
-#if NA_CHACHA_RUNS
         uint32_t xs[2][16];
-        solo_blocks2(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1]);
-#endif
+        if constexpr (RUNS) solo_blocks2<true>(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1], 2 * m < q.S);
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u; /* unit, ChaCha block j + 1 */
             if (j < q.J) {
                 uint32_t x[16], w[16];
-#if NA_CHACHA_RUNS
+                if constexpr (RUNS) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
-#else
-                chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
-#endif
+                    for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
+                } else {
+                    chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+                }
                 uint32_t nb = 4;
                 if constexpr (MODE == SOLO_OPEN1) {
 #pragma unroll
@@ -1284,7 +1291,7 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
     }
 }
 
-template <bool UKEY>
+template <bool UKEY, bool RUNS>
 NA_DEV void seal_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_job)
 {
     const SoloRec q = solo_rec(a, wave_job);
@@ -1297,7 +1304,7 @@ NA_DEV void seal_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
     uint32_t s[4];
     P32 h;
     solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, q.rc) : nullptr, a.ad_len, r, s, h);
-    solo_pass<SOLO_SEAL>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
+    solo_pass<SOLO_SEAL, RUNS>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
     uint32_t tag[4];
     solo_tag(h, r, a.ad_len, q.len, s, tag);
     if (q.live) tag_out(u_dst(a, q.rc) + q.len, q.len, tag);
@@ -1324,7 +1331,11 @@ NA_DEV void solo_auth(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the tile is read before the DMA refills it */
         __builtin_amdgcn_wave_barrier();
         if (m + 2 < q.S) solo_dma(a, q.rec0, q.lane, m + 2, q.lim, cur);
+        #ifdef NA_AUTH_PRIO_LVL /* A/B */
+        __builtin_amdgcn_s_setprio(NA_AUTH_PRIO_LVL);
+#else
         __builtin_amdgcn_s_setprio(3);
+#endif
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u;
@@ -1352,6 +1363,7 @@ NA_DEV void solo_auth(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
    rounds (profiles/r05/dec_rev_ab.txt; the forward pass is NA_DEC_REV=0 at
    the ab-arms-r5 revision, tools/ab/README.md); the last steps read by the
    AUTH pass are also the likeliest still in L2. */
+template <bool RUNS>
 NA_DEV void solo_dec_rev(const UniformArgs &a, const SoloRec &q, uint4 *tiles, const uint32_t key[8],
                          const ChaPre &pre, uint32_t n_lo, uint32_t n_hi, uint32_t okm, bool ok)
 {
@@ -1366,21 +1378,19 @@ NA_DEV void solo_dec_rev(const UniformArgs &a, const SoloRec &q, uint4 *tiles, c
         __builtin_amdgcn_wave_barrier();
         if (k >= 1 && m >= 1) solo_dma(a, q.rec0, q.lane, m - 1, q.lim, nxt); /* k = 0: step S-2 is there */
         prio_by_progress(k, q.S);
-#if NA_CHACHA_RUNS
         uint32_t xs[2][16];
-        solo_blocks2(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1]);
-#endif
+        if constexpr (RUNS) solo_blocks2<true>(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1], 2 * k < q.S);
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u;
             if (j < q.J) {
                 uint32_t x[16], w[16];
-#if NA_CHACHA_RUNS
+                if constexpr (RUNS) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
-#else
-                chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
-#endif
+                    for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
+                } else {
+                    chacha20_block_pre(key, pre, j + 1, n_lo, n_hi, x);
+                }
 #pragma unroll
                 for (int i = 0; i < 16; ++i) w[i] = wu[u][i] ^ x[i];
                 if (j == q.J - 1 && q.live && ok) last_unit_out(u_dst(a, q.rc) + q.full_lim, q.tail, w);
@@ -1404,7 +1414,7 @@ NA_DEV void solo_dec_rev(const UniformArgs &a, const SoloRec &q, uint4 *tiles, c
    open_il_staged does (in place: XOR with the key stream once more; out of
    place: zeroed).  The DEC pass reads the ciphertext
    again, mostly from L2 / MALL (a wave's 64 records are ~90 KB). */
-template <bool UKEY>
+template <bool UKEY, bool RUNS>
 NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_job)
 {
     const SoloRec q = solo_rec(a, wave_job);
@@ -1421,7 +1431,7 @@ NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
     P32 h;
     solo_poly_key(key, pre, n_lo, n_hi, a.ad_len ? u_ad(a, rc) : nullptr, a.ad_len, r, s, h);
     if (a.vf) solo_auth(a, q, tiles, r, h);
-    else solo_pass<SOLO_OPEN1>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
+    else solo_pass<SOLO_OPEN1, RUNS>(a, q, tiles, key, pre, n_lo, n_hi, r, h);
     uint32_t tag[4], got[4];
     solo_tag(h, r, a.ad_len, len, s, tag);
     tag_in<true>(u_src(a, rc), len, got); /* the tag bytes are never written */
@@ -1438,7 +1448,7 @@ NA_DEV void open_solo_staged(const UniformArgs &a, uint4 *tiles, uint32_t wave_j
         for (int i = 0; i < 8; ++i)
             okm |= (__shfl((int)ok, (int)(8u * i + (lane >> 3)), 64) != 0 ? 1u : 0u) << i;
         __builtin_amdgcn_wave_barrier(); /* the AUTH pass's tile reads are done */
-        solo_dec_rev(a, q, tiles, key, pre, n_lo, n_hi, okm, ok);
+        solo_dec_rev<RUNS>(a, q, tiles, key, pre, n_lo, n_hi, okm, ok);
         return;
     }
     const bool bad = live && !ok;
@@ -1769,18 +1779,20 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_duplex_staged(
    each; 256 records per workgroup. */
 #define NA_SOLO_OCC __attribute__((amdgpu_waves_per_eu(2)))
 
-template <bool UKEY>
+/* RUNS: the key stream in runs (solo_blocks2) — for launches of at least
+   two waves per SIMD (launch_chacha.hip picks) */
+template <bool UKEY, bool RUNS>
 __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_seal_solo(UniformArgs a)
 {
     __shared__ uint4 tiles[4][2 * SOLO_TILE];
-    seal_solo_staged<UKEY>(a, tiles[threadIdx.x >> 6], wave_of(blockIdx.x));
+    seal_solo_staged<UKEY, RUNS>(a, tiles[threadIdx.x >> 6], wave_of(blockIdx.x));
 }
 
-template <bool UKEY>
+template <bool UKEY, bool RUNS>
 __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_open_solo(UniformArgs a)
 {
     __shared__ uint4 tiles[4][2 * SOLO_TILE];
-    open_solo_staged<UKEY>(a, tiles[threadIdx.x >> 6], wave_of(blockIdx.x));
+    open_solo_staged<UKEY, RUNS>(a, tiles[threadIdx.x >> 6], wave_of(blockIdx.x));
 }
 
 /* chachapoly_duplex_staged's two-job launch over the one-lane kernels */
@@ -1810,8 +1822,8 @@ __global__ __launch_bounds__(256) NA_SOLO_OCC void chachapoly_duplex_solo(
         open = o_blocks > s_blocks;
         b -= n;
     }
-    if (open) open_solo_staged<UKEY>(o, tiles[threadIdx.x >> 6], wave_of(b));
-    else seal_solo_staged<UKEY>(s, tiles[threadIdx.x >> 6], wave_of(b));
+    if (open) open_solo_staged<UKEY, true>(o, tiles[threadIdx.x >> 6], wave_of(b));
+    else seal_solo_staged<UKEY, true>(s, tiles[threadIdx.x >> 6], wave_of(b));
 }
 
 template <int K, bool FAST>

@@ -467,12 +467,19 @@ NA_DEV void seg_step(const SegLane &q, const IO &io, uint32_t lane, uint32_t m, 
             solo_put(cur, lane, 1, wu[1]);
         }
     } else {
+        /* both blocks in lock step, issued in runs (chachapoly.hip
+           solo_blocks2: the persistent and the K = 2 kernels hold two waves
+           per SIMD) */
+        uint32_t xs[2][16];
+        if (2 * m < q.nb && (MODE != SEG_DEC || ok))
+            solo_blocks2<true>(key, pre, q.b0 + 2 * m, q.n_lo, q.n_hi, xs[0], xs[1]);
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t blk = q.b0 + 2 * m + u;
             if (2 * m + u < q.nb && blk != 0 && (MODE != SEG_DEC || ok)) {
                 uint32_t x[16], nbp;
-                chacha20_block_pre(key, pre, blk, q.n_lo, q.n_hi, x);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = xs[u][i];
                 seg_data<MODE>(q, blk - 1, wu[u], x, r, h, ok, nbp);
                 solo_put(cur, lane, u, wu[u]);
             }

@@ -39,14 +39,19 @@ KernelFn<UniformArgs> chacha_staged_fn(bool open, bool ukey)
    (open_solo_staged) or the two-pass chachapoly_open_uniform, never the
    one-pass 4/8-lane staged kernels */
 template <bool FAST>
-KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf)
+KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf, bool runs)
 {
     switch (k) {
     case 1:
-        /* one lane per record, LDS-staged (seal_solo_staged) */
+        /* one lane per record, LDS-staged (seal_solo_staged); runs: the key
+           stream issued in runs once the launch holds two waves per SIMD */
         if (FAST) {
-            if (ukey) return open ? chachapoly_open_solo<true> : chachapoly_seal_solo<true>;
-            return open ? chachapoly_open_solo<false> : chachapoly_seal_solo<false>;
+            if (runs) {
+                if (ukey) return open ? chachapoly_open_solo<true, true> : chachapoly_seal_solo<true, true>;
+                return open ? chachapoly_open_solo<false, true> : chachapoly_seal_solo<false, true>;
+            }
+            if (ukey) return open ? chachapoly_open_solo<true, false> : chachapoly_seal_solo<true, false>;
+            return open ? chachapoly_open_solo<false, false> : chachapoly_seal_solo<false, false>;
         }
         return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
     case 2: return open ? chachapoly_open_uniform<2, FAST> : chachapoly_seal_uniform<2, FAST>;
@@ -64,10 +69,10 @@ KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf)
 }
 
 /* ukey: every wave's 64/k records share one state (see u_key_nonce) */
-KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast, bool ukey, bool vf)
+KernelFn<UniformArgs> chacha_uniform_fn(int k, bool open, bool fast, bool ukey, bool vf, bool runs)
 {
-    return fast ? chacha_uniform_fn_t<true>(k, open, ukey, vf)
-                : chacha_uniform_fn_t<false>(k, open, ukey, vf);
+    return fast ? chacha_uniform_fn_t<true>(k, open, ukey, vf, runs)
+                : chacha_uniform_fn_t<false>(k, open, ukey, vf, runs);
 }
 
 /* VF: the FAST opens' two-pass (verify-first) instantiation; the generic
@@ -108,6 +113,21 @@ uint32_t resident_blocks(F fn)
 
 } // namespace
 
+/* the current device's CU count, cached per device (0: unknown) */
+static uint32_t duplex_run_chunk_cus()
+{
+    constexpr int MAX_DEV = 64;
+    static std::atomic<uint32_t> cache[MAX_DEV];
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= MAX_DEV) return 0;
+    uint32_t v = cache[dev].load(std::memory_order_relaxed);
+    if (!v && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+        v = (uint32_t)cus;
+        cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
+
 int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, bool ukey, hipStream_t s)
 {
     if (k == 2 && fast) {
@@ -117,7 +137,11 @@ int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, bool ukey,
                                         : (uk ? chachapoly_seg2_uniform<false, true> : chachapoly_seg2_uniform<false, false>);
         return launch(fn, a.n_records, 2, a, s);
     }
-    KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, fast, ukey, a.vf != 0);
+    /* one lane per record: runs once the launch is two waves per SIMD
+       (64 records per wave, four SIMDs per CU) */
+    const uint32_t cus = duplex_run_chunk_cus();
+    const bool runs = cus && (uint64_t)a.n_records >= 2ull * 4 * 64 * cus;
+    KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, fast, ukey, a.vf != 0, runs);
     if (!fn) return NOISE_ERROR_INVALID_PARAM;
     return launch(fn, a.n_records, k, a, s);
 }

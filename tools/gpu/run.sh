@@ -10,7 +10,7 @@
 #                                #   summaries of the timed window (tools/kernel_window.py)
 #   pmc    NAME  CFG ARGS...     # PMC passes of bench.py --config CFG ARGS (tools/gpu/pmc.sh),
 #                                #   summarised to NAME.traffic.json (tools/pmc_report.py)
-#   ab     NAME  ROUNDS  LIBS  -- ARGS...
+#   ab     NAME  ROUNDS  LIB...  -- ARGS...
 #                                # interleaved A/B: for each round, each library variant
 #                                #   (cur = the in-tree library, X = noise-c_amd/ab/libnoise_aead_hip_X.so)
 #                                #   runs bench.py ARGS -> NAME.jsonl
@@ -95,7 +95,10 @@ PY
       head -20 "$O/$name.pmc.txt"
     else echo "pmc $name rc=$rc"; tail -5 "$O/pmc_$name.log"; fi ;;
   ab)
-    local name=$1 rounds=$2 libs=$3; shift 3; [ "${1:-}" = "--" ] && shift
+    local name=$1 rounds=$2; shift 2
+    local libs=""
+    while [ $# -gt 0 ] && [ "$1" != "--" ]; do libs="$libs $1"; shift; done
+    [ "${1:-}" = "--" ] && shift
     local i v
     for i in $(seq "$rounds"); do
       for v in $libs; do
@@ -134,8 +137,8 @@ PY
 
 while read -r line; do
   case "$line" in ''|'#'*) continue;; esac
-  # shellcheck disable=SC2086
-  set -- $line
+  # the line's words, shell quoting honoured ("-k 'a or b'")
+  eval "set -- $line"
   step "$@" < /dev/null
   rc=$?
   if [ $rc -ne 0 ]; then

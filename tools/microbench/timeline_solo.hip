@@ -40,8 +40,8 @@ __global__ __launch_bounds__(256) NA_SOLO_OCC void timed(UniformArgs s, UniformA
         open = ob > sb;
         b -= n;
     }
-    if (open) open_solo_staged<true>(o, tiles[threadIdx.x >> 6], wave_of(b));
-    else seal_solo_staged<true>(s, tiles[threadIdx.x >> 6], wave_of(b));
+    if (open) open_solo_staged<true, true>(o, tiles[threadIdx.x >> 6], wave_of(b));
+    else seal_solo_staged<true, true>(s, tiles[threadIdx.x >> 6], wave_of(b));
     const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0) {
         Stamp x;
@@ -80,7 +80,7 @@ int main(int argc, char **argv)
         hipMemset(pa, 0x5a + k, (size_t)N * SI);
         UniformArgs sa{key, nb, pa, ca, nullptr, nullptr, SI, SO, 0, N, N, L, 0, 0, 0};
         UniformArgs sb{key, nb, pa, cb, nullptr, nullptr, SI, SO, 0, N, N, L, 0, 0, 0};
-        hipLaunchKernelGGL((chachapoly_seal_solo<true>), dim3(N / 256), dim3(256), 0, 0, sb);
+        hipLaunchKernelGGL((chachapoly_seal_solo<true, true>), dim3(N / 256), dim3(256), 0, 0, sb);
         UniformArgs ob{key, nb, cb, back, nullptr, stt, SO, SI, 0, N, N, L, 0, 0, (uint32_t)vf};
         SA.push_back(sa);
         OB.push_back(ob);
