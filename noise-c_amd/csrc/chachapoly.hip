@@ -1204,17 +1204,20 @@ NA_DEV SoloRec solo_rec(const UniformArgs &a, uint32_t wave_job)
    C5 +5 %; toggles 3 / 1 measured the same, runs without the toggles
    nothing.  A standalone one-lane launch of < 2 waves per SIMD lost 11 %
    with it (a lone wave has no partner to fill the slots a rotate run
-   leaves), so those keep hipcc's schedule (RUNS = false). */
+   leaves), so those keep hipcc's schedule (RUNS = false).
+   early (a launch of one generation, UniformArgs.balance, in the first half
+   of the wave's steps): the toggles one level up, 3 / 1 — the progress
+   balance of prio_by_progress, which the toggles override, in two levels:
+   C2 duplex 1497-1530 -> 1555-1612 GiB/s in three interleaved rounds, while
+   with it at C4 (16 generations) 1736-1741 -> 1716-1726, hence the
+   one-generation condition (profiles/r06/prio_ab/). */
 template <bool RUNS>
 NA_DEV void solo_blocks2(const uint32_t key[8], const ChaPre &pre, uint32_t c0, uint32_t n_lo, uint32_t n_hi,
                          uint32_t (&x0)[16], uint32_t (&x1)[16], bool early = false)
 {
     if constexpr (RUNS) {
-#ifdef NA_RUNS_PROGRESS /* A/B: a wave in the first half of its steps one level up */
         if (early) chacha20_2block_runs<3, 1, 1>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
-        else
-#endif
-        chacha20_2block_runs<2, 0, 0>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
+        else chacha20_2block_runs<2, 0, 0>(key, pre, c0, c0 + 1, n_lo, n_hi, x0, x1);
     } else {
         chacha20_block_pre(key, pre, c0, n_lo, n_hi, x0);
         chacha20_block_pre(key, pre, c0 + 1, n_lo, n_hi, x1);
@@ -1247,7 +1250,7 @@ NA_DEV void solo_pass(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
            (profiles/r04/solo_prio_ab.jsonl). */
         prio_by_progress(m, q.S);
         uint32_t xs[2][16];
-        if constexpr (RUNS) solo_blocks2<true>(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1], 2 * m < q.S);
+        if constexpr (RUNS) solo_blocks2<true>(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1], a.balance && 2 * m < q.S);
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u; /* unit, ChaCha block j + 1 */
@@ -1331,11 +1334,7 @@ NA_DEV void solo_auth(const UniformArgs &a, const SoloRec &q, uint4 *tiles, cons
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the tile is read before the DMA refills it */
         __builtin_amdgcn_wave_barrier();
         if (m + 2 < q.S) solo_dma(a, q.rec0, q.lane, m + 2, q.lim, cur);
-        #ifdef NA_AUTH_PRIO_LVL /* A/B */
-        __builtin_amdgcn_s_setprio(NA_AUTH_PRIO_LVL);
-#else
-        __builtin_amdgcn_s_setprio(3);
-#endif
+                __builtin_amdgcn_s_setprio(3);
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u;
@@ -1379,7 +1378,7 @@ NA_DEV void solo_dec_rev(const UniformArgs &a, const SoloRec &q, uint4 *tiles, c
         if (k >= 1 && m >= 1) solo_dma(a, q.rec0, q.lane, m - 1, q.lim, nxt); /* k = 0: step S-2 is there */
         prio_by_progress(k, q.S);
         uint32_t xs[2][16];
-        if constexpr (RUNS) solo_blocks2<true>(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1], 2 * k < q.S);
+        if constexpr (RUNS) solo_blocks2<true>(key, pre, 2 * m + 1, n_lo, n_hi, xs[0], xs[1], a.balance && 2 * k < q.S);
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = 2 * m + u;

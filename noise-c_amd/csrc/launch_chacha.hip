@@ -143,6 +143,13 @@ int chacha_uniform(const UniformArgs &a, int k, bool open, bool fast, bool ukey,
     const bool runs = cus && (uint64_t)a.n_records >= 2ull * 4 * 64 * cus;
     KernelFn<UniformArgs> fn = chacha_uniform_fn(k, open, fast, ukey, a.vf != 0, runs);
     if (!fn) return NOISE_ERROR_INVALID_PARAM;
+    if (k == 1 && fast) {
+        /* one-lane kernels: balance = the launch is one generation (at most
+           two 64-record waves per SIMD; chachapoly.hip solo_blocks2) */
+        UniformArgs b = a;
+        b.balance = cus && (uint64_t)a.n_records <= 2ull * 4 * 64 * cus;
+        return launch(fn, a.n_records, k, b, s);
+    }
     return launch(fn, a.n_records, k, a, s);
 }
 
@@ -168,9 +175,14 @@ int chacha_duplex(const UniformArgs &a, const UniformArgs &b, int k, bool ukey, 
     const uint32_t sb = (uint32_t)(((uint64_t)a.n_records * k + 255) / 256);
     const uint32_t ob = (uint32_t)(((uint64_t)b.n_records * k + 255) / 256);
     if (k == 1) {
+        /* balance: the launch is one generation (two waves per SIMD at most,
+           256-thread blocks of four waves; chachapoly.hip solo_blocks2) */
+        const uint32_t cus = duplex_run_chunk_cus();
+        UniformArgs a1 = a, b1 = b;
+        a1.balance = b1.balance = cus && (uint64_t)(sb + ob) <= 2ull * cus;
         worker_park_for_batch(sb + ob);
         hipLaunchKernelGGL(ukey ? chachapoly_duplex_solo<true> : chachapoly_duplex_solo<false>, dim3(sb + ob),
-                           dim3(256), 0, s, a, b, sb, ob, duplex_run_chunk());
+                           dim3(256), 0, s, a1, b1, sb, ob, duplex_run_chunk());
         return hip_rc(hipGetLastError());
     }
     void (*fn)(UniformArgs, UniformArgs, uint32_t, uint32_t);

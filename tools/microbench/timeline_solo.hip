@@ -78,10 +78,10 @@ int main(int argc, char **argv)
         hipMalloc(&pa, (size_t)N * SI + 4096); hipMalloc(&ca, (size_t)N * SO + 4096);
         hipMalloc(&cb, (size_t)N * SO + 4096); hipMalloc(&back, (size_t)N * SI + 4096);
         hipMemset(pa, 0x5a + k, (size_t)N * SI);
-        UniformArgs sa{key, nb, pa, ca, nullptr, nullptr, SI, SO, 0, N, N, L, 0, 0, 0};
+        UniformArgs sa{key, nb, pa, ca, nullptr, nullptr, SI, SO, 0, N, N, L, 0, 1, 0}; /* balance: one generation, as the library sets it */
         UniformArgs sb{key, nb, pa, cb, nullptr, nullptr, SI, SO, 0, N, N, L, 0, 0, 0};
         hipLaunchKernelGGL((chachapoly_seal_solo<true, true>), dim3(N / 256), dim3(256), 0, 0, sb);
-        UniformArgs ob{key, nb, cb, back, nullptr, stt, SO, SI, 0, N, N, L, 0, 0, (uint32_t)vf};
+        UniformArgs ob{key, nb, cb, back, nullptr, stt, SO, SI, 0, N, N, L, 0, 1, (uint32_t)vf};
         SA.push_back(sa);
         OB.push_back(ob);
     }
