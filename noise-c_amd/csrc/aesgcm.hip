@@ -673,56 +673,6 @@ NA_DEV AesPre aes_pre_lds(const uint8_t *L, RK rk, uint32_t tpl, uint32_t n_hi,
     return p;
 }
 
-#ifdef NA_AES_RUNS
-/* A/B (round 6): one AES round with its VALU in runs — the 16 lookup
-   addresses (v_perm_b32, slow class) at s_setprio 2, the 16 LDS lookups,
-   then the column XORs (v_bitop3_b32, fast class) at s_setprio 0, pinned by
-   inline asm (the ChaCha finding of aead_device.h chacha20_2block_runs). */
-NA_DEV void aes_perm4(uint32_t s, uint32_t tpl, uint32_t &a0, uint32_t &a1, uint32_t &a2, uint32_t &a3)
-{
-    /* te_lookup's selectors for (TAB, K) = (0,3) (1,2) (2,1) (3,0) */
-    constexpr uint32_t S0 = (0x0cu << 24) | (0x0cu << 16) | (7u << 8) | 0u;
-    constexpr uint32_t S1 = (0x0cu << 24) | (0x0cu << 16) | (6u << 8) | 1u;
-    constexpr uint32_t S2 = (0x0cu << 24) | (2u << 16) | (5u << 8) | 0u;
-    constexpr uint32_t S3 = (0x0cu << 24) | (2u << 16) | (4u << 8) | 1u;
-    asm volatile("v_perm_b32 %0, %4, %5, %6\n\tv_perm_b32 %1, %4, %5, %7\n\t"
-                 "v_perm_b32 %2, %4, %5, %8\n\tv_perm_b32 %3, %4, %5, %9"
-                 : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
-                 : "v"(s), "v"(tpl), "s"(S0), "s"(S1), "s"(S2), "s"(S3));
-}
-
-NA_DEV uint32_t xor5_asm(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k)
-{
-    uint32_t t, r;
-    asm volatile("v_bitop3_b32 %0, %2, %3, %4 bitop3:0x96\n\tv_bitop3_b32 %1, %0, %5, %6 bitop3:0x96"
-                 : "=&v"(t), "=&v"(r) : "v"(a), "v"(b), "v"(c), "v"(d), "v"(k));
-    return r;
-}
-
-template <typename RK>
-NA_DEV void aes_round_runs(const uint8_t *L, RK rk, int r, uint32_t tpl, uint32_t &s0, uint32_t &s1,
-                           uint32_t &s2, uint32_t &s3)
-{
-    uint32_t a[4][4]; /* a[t][j]: table t's address for state word j */
-    __builtin_amdgcn_s_setprio(2);
-    aes_perm4(s0, tpl, a[0][0], a[1][0], a[2][0], a[3][0]);
-    aes_perm4(s1, tpl, a[0][1], a[1][1], a[2][1], a[3][1]);
-    aes_perm4(s2, tpl, a[0][2], a[1][2], a[2][2], a[3][2]);
-    aes_perm4(s3, tpl, a[0][3], a[1][3], a[2][3], a[3][3]);
-    uint32_t v[4][4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) v[c][t] = *(const uint32_t *)(L + a[t][(c + t) & 3]);
-    const uint32_t k0 = rk[4 * r], k1 = rk[4 * r + 1], k2 = rk[4 * r + 2], k3 = rk[4 * r + 3];
-    __builtin_amdgcn_s_setprio(0);
-    s0 = xor5_asm(v[0][0], v[0][1], v[0][2], v[0][3], k0);
-    s1 = xor5_asm(v[1][0], v[1][1], v[1][2], v[1][3], k1);
-    s2 = xor5_asm(v[2][0], v[2][1], v[2][2], v[2][3], k2);
-    s3 = xor5_asm(v[3][0], v[3][1], v[3][2], v[3][3], k3);
-}
-#endif
-
 /* E_K(0^32 || BE64(n) || BE32(ctr)) from the record's AesPre (ctr < 2^16),
    as little-endian memory words; equals aes_ctr_lds. */
 template <typename RK>
@@ -736,10 +686,6 @@ NA_DEV void aes_ctr_pre(const uint8_t *L, RK rk, uint32_t tpl, const AesPre &p,
     uint32_t s1 = xor3(p.d1, te_lookup<0, 3>(L, t1, tpl), te_lookup<3, 0>(L, t0, tpl));
     uint32_t s2 = xor3(p.d2, te_lookup<2, 1>(L, t0, tpl), te_lookup<3, 0>(L, t1, tpl));
     uint32_t s3b = xor3(p.d3, te_lookup<1, 2>(L, t0, tpl), te_lookup<2, 1>(L, t1, tpl));
-#ifdef NA_AES_RUNS
-#pragma unroll
-    for (int r = 3; r < 14; ++r) aes_round_runs(L, rk, r, tpl, s0, s1, s2, s3b);
-#else
 #pragma unroll
     for (int r = 3; r < 14; ++r) {
 #define NA_COL(a, b, c, d, k)                                                        \
@@ -753,7 +699,6 @@ NA_DEV void aes_ctr_pre(const uint8_t *L, RK rk, uint32_t tpl, const AesPre &p,
 #undef NA_COL
         s0 = u0; s1 = u1; s2 = u2; s3b = u3;
     }
-#endif
 #define NA_SB4(a, b, c, d)                                                          \
     ((te_lookup<2, 3>(L, a, tpl) & 0xff000000u) | (te_lookup<3, 2>(L, b, tpl) & 0x00ff0000u) | \
      (te_lookup<0, 1>(L, c, tpl) & 0x0000ff00u) | (te_lookup<1, 0>(L, d, tpl) & 0x000000ffu))
