@@ -763,11 +763,13 @@ NA_DEV void wave_store(const UniformArgs &a, const WaveIO<K> &io, int j0, int la
     const int u = j0 + io.kk;
     if (u < 0 || u > last_full) return;
     const uint32_t off = io.c16 + 64u * (uint32_t)u;
+    uint4 q[4]; /* all tile reads first: one LDS wait, not one per store (solo_store) */
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = t[tile_slot(16u * i + (lane >> 2), lane & 3)];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const uint4 q = t[tile_slot(16u * i + (lane >> 2), lane & 3)];
         const uint32_t r = wave_rec(io, i);
-        if (r < a.n_records && ((okm >> i) & 1)) rec_store16(a.out + (size_t)r * a.out_stride + off, q);
+        if (r < a.n_records && ((okm >> i) & 1)) rec_store16(a.out + (size_t)r * a.out_stride + off, q[i]);
     }
 }
 
@@ -1114,15 +1116,23 @@ NA_DEV void solo_store(const UniformArgs &a, uint32_t rec0, uint32_t lane, uint3
 {
     const uint32_t off = 128u * m + 16u * solo_chunk(lane);
     if (off + 16u > full_lim) return;
+    /* The eight tile reads first and one wait for them: with a read inside
+       each conditional store hipcc waited on every read in turn (eight LDS
+       round trips per step).  The explicit wait also orders the reads before
+       the caller's next LDS-DMA into this tile (dma16_asm: hipcc does not
+       see that write). */
+    uint4 q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = t[64 * i + lane];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint4 q = t[64 * i + lane];
         const uint32_t r = rec0 + 8u * i + (lane >> 3);
         /* non-temporal (rec_store16): the one-lane kernels' store pattern
            (8 x 128 B per instruction) alone runs at 4.9 vs 3.8 TB/s, and C4 /
            perf gain 1-3 % (tools/microbench/solo_dma.hip,
            profiles/r04/nt_store_ab.jsonl) */
-        if (r < a.n_records && ((okm >> i) & 1)) rec_store16(a.out + (size_t)r * a.out_stride + off, q);
+        if (r < a.n_records && ((okm >> i) & 1)) rec_store16(a.out + (size_t)r * a.out_stride + off, q[i]);
     }
 }
 
