@@ -14,8 +14,9 @@
 #                                # interleaved A/B: for each round, each library variant
 #                                #   (cur = the in-tree library, X = noise-c_amd/ab/libnoise_aead_hip_X.so)
 #                                #   runs bench.py ARGS -> NAME.jsonl
-#   abargs NAME  ROUNDS  -- ARGS_A  ||  ARGS_B  [|| ARGS_C ...]
+#   abargs NAME  ROUNDS  -- ARGS_A  ::  ARGS_B  [:: ARGS_C ...]
 #                                # interleaved A/B of bench argument sets on the in-tree library
+#                                #   (a set may start with VAR=value words: its environment)
 #   cmd    NAME  SECONDS  COMMAND...   # any command, its own time limit, output NAME.log
 #   EOF
 #
@@ -114,13 +115,17 @@ PY
     local name=$1 rounds=$2; shift 2; [ "${1:-}" = "--" ] && shift
     local sets=() cur="" a i k
     for a in "$@"; do
-      if [ "$a" = "||" ]; then sets+=("$cur"); cur=""; else cur="$cur $a"; fi
+      if [ "$a" = "::" ]; then sets+=("$cur"); cur=""; else cur="$cur $a"; fi
     done
     sets+=("$cur")
     for i in $(seq "$rounds"); do
       for k in "${!sets[@]}"; do
-        # shellcheck disable=SC2086
-        timeout -k 10 400 python bench.py ${sets[$k]} > "$O/$name.$k.$i.json" 2> "$O/$name.$k.$i.err" || rc=$?
+        # leading VAR=value words of a set are its environment
+        local envs=() args=() w
+        for w in ${sets[$k]}; do
+          if [ ${#args[@]} -eq 0 ] && [[ "$w" == [A-Z]*=* ]]; then envs+=("$w"); else args+=("$w"); fi
+        done
+        timeout -k 10 400 env "${envs[@]}" python bench.py "${args[@]}" > "$O/$name.$k.$i.json" 2> "$O/$name.$k.$i.err" || rc=$?
         if [ $rc -ne 0 ]; then echo "abargs $name $k rc=$rc"; tail -5 "$O/$name.$k.$i.err"; fatal $rc && return $rc; rc=0; continue; fi
         python3 -c "import json;d=json.loads(open('$O/$name.$k.$i.json').read().strip().splitlines()[-1]);d['ab']={'args':'''${sets[$k]}''','round':$i};print(json.dumps(d))" >> "$O/$name.jsonl"
         summ "$name [${sets[$k]} ] r$i" "$O/$name.$k.$i.json"
