@@ -244,10 +244,11 @@ int run_uniform(int cipher_id, const NoiseAeadUniform *job, void *stream, bool o
     if (cipher_id == NOISE_CIPHER_CHACHAPOLY) {
         const int k = uniform_lanes(job, open, false);
         const bool ukey = (k >= 4 || k == 1) && job->recs_per_state % (64u / (uint32_t)k) == 0;
-        /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC): open
-           balances its waves' progress (profiles/r01_prio_ab.jsonl); in the
-           seal it measured neutral (profiles/r02/timeline_c2_seal_open_duplex.log) */
-        a.balance = open && (uint64_t)job->n_records * (uint32_t)k <= 4096ull * 64;
+        /* 4 resident waves on each of 1024 SIMDs (NA_UNIFORM_OCC): one
+           generation balances its waves' progress (open: profiles/r01_prio_ab
+           .jsonl; seal: neutral in round 2, +3-8 % once the key stream ran in
+           runs, the early toggles of chachapoly.hip slot_block) */
+        a.balance = (uint64_t)job->n_records * (uint32_t)k <= 4096ull * 64;
         return chacha_uniform(a, k, open, uniform_fast(job, open), ukey, s);
     }
     if (cipher_id == NOISE_CIPHER_AESGCM) {

@@ -381,18 +381,25 @@ NA_DEV void poly_tree_close(Fe acc, int k, const Fe &r, const Mul &mr, uint32_t 
    kernels: four waves per SIMD) issues the block in runs with priority
    toggles (aead_device.h chacha20_block_runs, round 6); the windowed
    kernels, whose small batches often hold under one wave per SIMD, keep
-   hipcc's schedule. */
+   hipcc's schedule.  early (a one-generation launch, UniformArgs.balance,
+   in the first half of the wave's steps): toggles 3 / 1, the progress
+   balance of solo_blocks2 — the standalone C2 seal 55.5-60.1 -> 54.1-55.3
+   us per launch in four interleaved rounds (profiles/r06/staged_early_ab/). */
 template <bool RUNS = false>
 NA_DEV void slot_block(const uint32_t key[8], const ChaPre &pre, int v, uint32_t n_lo,
-                       uint32_t n_hi, uint32_t x[16])
+                       uint32_t n_hi, uint32_t x[16], bool early = false)
 {
     if (v < 0) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = 0;
         return;
     }
-    if constexpr (RUNS) chacha20_block_runs<2, 0, 0>(key, pre, (uint32_t)v, n_lo, n_hi, x);
-    else chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+    if constexpr (RUNS) {
+        if (early) chacha20_block_runs<3, 1, 1>(key, pre, (uint32_t)v, n_lo, n_hi, x);
+        else chacha20_block_runs<2, 0, 0>(key, pre, (uint32_t)v, n_lo, n_hi, x);
+    } else {
+        chacha20_block_pre(key, pre, (uint32_t)v, n_lo, n_hi, x);
+    }
 }
 
 template <int K, bool FAST>
@@ -883,7 +890,7 @@ NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
         /* next step's bytes go into the other tile while this one computes */
         if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
-        slot_block<true>(key, pre, v, n_lo, n_hi, x);
+        slot_block<true>(key, pre, v, n_lo, n_hi, x, a.balance && 2 * m < g.steps);
         if (m == 0) {
             Fe r;
             poly_key_bcast(x, gbase + (int)g.o, r, s);
@@ -963,7 +970,7 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
         __builtin_amdgcn_wave_barrier();
         if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
-        slot_block<true>(key, pre, v, n_lo, n_hi, x);
+        slot_block<true>(key, pre, v, n_lo, n_hi, x, a.balance && 2 * m < g.steps);
         if (m == 0) {
             Fe r;
             poly_key_bcast(x, gbase + (int)g.o, r, s);
