@@ -66,9 +66,11 @@ bool uniform_fast(const NoiseAeadUniform *j, bool open)
    SOLO_MIN_STANDALONE records, two waves per SIMD: C4's 1 Mi records as
    back-to-back seal and open launches 1624-1636 vs 1410-1415 GiB/s at four
    lanes, while a 64 Ki-record job alone (one wave per SIMD) runs 3 % faster
-   at four lanes (1315-1321 vs 1280-1283, profiles/r04/separate_lanes_ab.jsonl)
-   — except a verify-first open (the default), which the 4/8-lane staged
-   kernels do not run.  NOISE_AEAD_SOLO=0 keeps the 4-lane kernels everywhere (A/B runs). */
+   at four lanes (1315-1321 vs 1280-1283, profiles/r04/separate_lanes_ab.jsonl);
+   a verify-first open (the default) too since round 6's 4/8-lane
+   verify-first staged kernel (chachapoly.hip open_il_staged_vf): 1388-1389
+   vs 1236-1262 GiB/s at 64 Ki x 1400 B (profiles/r06/vf_staged_ab/).
+   NOISE_AEAD_SOLO=0 keeps the 4-lane kernels everywhere (A/B runs). */
 constexpr uint32_t SOLO_MIN_RECORDS = 65536;
 constexpr uint32_t SOLO_MIN_STANDALONE = 2 * SOLO_MIN_RECORDS;
 
@@ -110,8 +112,6 @@ int standalone_lanes(uint32_t n)
     return seg_mode() == 2 ? 2 : 0;
 }
 
-bool flags_vf(uint32_t flags);
-
 int uniform_lanes(const NoiseAeadUniform *j, bool open, bool duplex)
 {
     if (j->lanes_per_record) return (int)j->lanes_per_record;
@@ -119,7 +119,6 @@ int uniform_lanes(const NoiseAeadUniform *j, bool open, bool duplex)
         if (duplex) return 1;
         const int k = standalone_lanes(j->n_records);
         if (k) return k;
-        if (open && flags_vf(j->flags)) return 1;
     }
     return auto_lanes(j->n_records, 0);
 }

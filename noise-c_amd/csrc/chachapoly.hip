@@ -1746,6 +1746,135 @@ NA_DEV RecView ragged_view(const RaggedArgs &a, uint32_t rec)
 NA_DEV uint32_t wave_of(uint32_t b) { return (b * 256u + threadIdx.x) >> 6; }
 
 /* LDS-staged uniform FAST batches, K = 4 or 8 lanes per record */
+/* The staged kernels' coalesced step DMA (wave_dma) issued as inline asm
+   (dma16_asm): hipcc does not see these LDS writes, so it does not wait for
+   the youngest of them before every tile read; the caller waits itself
+   (s_waitcnt vmcnt: four instructions per step). */
+template <int K>
+NA_DEV void wave_dma_asm(const UniformArgs &a, const WaveIO<K> &io, int j0, uint4 *t)
+{
+    const int u = j0 + io.kk;
+    const uint32_t off = io.d16 + 64u * (uint32_t)(u > 0 ? u : 0);
+    const uint32_t last = a.n_records - 1;
+    const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        dma16_asm((const void *)(a.in + (size_t)min(wave_rec(io, i), last) * a.in_stride + off),
+                  base + 1024u * (uint32_t)i);
+}
+
+/* Verify-first open with K lanes per record (round 6): the reference's order
+   (cipher-chachapoly.c:135-141) at the staged kernels' four waves per SIMD,
+   for standalone opens (the one-lane verify-first open holds one wave per
+   SIMD at 64 Ki records).
+     AUTH: Poly1305 over the ciphertext only, the two tiles a two-step DMA
+           queue (inline-asm DMA, explicit waits), at top priority;
+     DEC:  verified waves only — the one-pass loop's key stream and XOR, the
+           stores gated per owner by the verdicts (okm), step 0's key stream
+           kept from the AUTH pass (its blocks gave r and s).
+   A rejected record's output is never written. */
+template <int K, bool UKEY>
+NA_DEV void open_il_staged_vf(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uint32_t wave_job)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t rec0 = wave_job * (64 / K);
+    const uint32_t rec_raw = rec0 + lane / K;
+    const bool live = rec_raw < a.n_records;
+    const uint32_t rc = live ? rec_raw : a.n_records - 1;
+    const int k = (int)(lane % K);
+    uint32_t key[8], n_lo, n_hi;
+    u_key_nonce<UKEY>(a, rec0, rc, key, n_lo, n_hi);
+    ChaPre pre;
+    chacha_pre(key, n_lo, n_hi, pre);
+    const uint32_t len = a.len;
+    const GroupCtx<K> g = group_ctx<K>(len);
+    const int gbase = (int)lane & ~(K - 1);
+    const WaveIO<K> io = wave_io<K>(rec0, lane);
+    const int last_full = (int)g.J - 2;
+    const uint32_t tail = g.J ? len - 64 * (g.J - 1) : 0; /* bytes of unit J-1 */
+
+    /* AUTH */
+    wave_dma_asm<K>(a, io, -(int)g.o - 1, tiles);
+    if (g.steps > 1) wave_dma_asm<K>(a, io, K - (int)g.o - 1, tiles + 256);
+    Fe acc = fe_zero();
+    Mul mr, mjump;
+    uint32_t s[4];
+    uint32_t x0[16]; /* step 0's blocks: the key block on one lane, data key stream on the others */
+    slot_block<true>(key, pre, k - (int)g.o, n_lo, n_hi, x0, a.balance != 0);
+    {
+        Fe r;
+        poly_key_bcast(x0, gbase + (int)g.o, r, s);
+        mr = mk_mul(r);
+        Mul mfinal;
+        poly_powers<K>(r, k, g.q, mjump, mfinal);
+        fin_put(fin, lane, mfinal);
+        const int k0 = g.J ? (int)((g.o + 1) % K) : K - 1;
+        if (k == k0 && a.ad_len) poly_ad(acc, mr, u_ad(a, rc), a.ad_len);
+    }
+    bool seen = false;
+    for (uint32_t m = 0; m < g.steps; ++m) {
+        const int j0 = (int)(m * K) - (int)g.o - 1;
+        const int v = j0 + 1 + k;
+        uint4 *cur = tiles + 256 * (m & 1);
+        if (m + 1 < g.steps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); /* this step's four, not the next's */
+        else solo_wait();
+        uint32_t w[16];
+        tile_get_unit(cur, lane, w);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* the tile is read before the DMA refills it */
+        __builtin_amdgcn_wave_barrier();
+        if (m + 2 < g.steps) wave_dma_asm<K>(a, io, j0 + 2 * K, cur);
+        __builtin_amdgcn_s_setprio(3);
+        if (v >= 1 && (uint32_t)v <= g.J) {
+            uint32_t nb = 4;
+            if ((uint32_t)v == g.J) {
+                mask_unit(w, tail);
+                nb = (tail + 15) / 16;
+            }
+            poly_unit(acc, seen ? mjump : mr, mr, w, nb);
+            seen = true;
+        }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    uint32_t tag[4], got[4];
+    poly_close<K>(acc, k, mr, fin_get(fin, lane), a.ad_len, len, s, tag);
+    tag_in<true>(u_src(a, rc), len, got); /* the tag bytes are never written */
+    const bool ok = tag_equal(tag, got);
+    if (k == K - 1 && live && a.status) a.status[rec_raw] = ok ? 0 : 1;
+    if (__ballot(live && ok) == 0) return;
+
+    /* DEC: bit i of okm = the owner coalesced instruction i serves is verified */
+    uint32_t okm = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        okm |= (__shfl((int)ok, (int)(16u * i + (lane >> 2)), 64) != 0 ? 1u : 0u) << i;
+    __builtin_amdgcn_wave_barrier(); /* the AUTH pass's tile reads are done */
+    wave_dma<K>(a, io, -(int)g.o - 1, tiles);
+    for (uint32_t m = 0; m < g.steps; ++m) {
+        if (a.balance) prio_by_progress(m, g.steps);
+        const int j0 = (int)(m * K) - (int)g.o - 1;
+        const int v = j0 + 1 + k;
+        uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
+        __builtin_amdgcn_wave_barrier();
+        if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
+        uint32_t x[16];
+        if (m == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = x0[i];
+        } else {
+            slot_block<true>(key, pre, v, n_lo, n_hi, x, a.balance && 2 * m < g.steps);
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t w[16];
+        tile_get_unit(cur, lane, w);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] ^= x[i];
+        if (v >= 1 && (uint32_t)v == g.J && live && ok) last_unit_out(u_dst(a, rc) + 64 * (g.J - 1), tail, w);
+        tile_put_unit(cur, lane, w);
+        __builtin_amdgcn_wave_barrier();
+        wave_store<K>(a, io, j0, last_full, cur, lane, okm);
+    }
+}
+
 template <int K, bool UKEY>
 __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_seal_staged(UniformArgs a)
 {
@@ -1760,6 +1889,15 @@ __global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_open_staged(Uni
     __shared__ uint4 tiles[4][512];
     __shared__ FinSlot fin[4];
     open_il_staged<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], wave_of(blockIdx.x));
+}
+
+/* verify-first (open_il_staged_vf) */
+template <int K, bool UKEY>
+__global__ __launch_bounds__(256) NA_UNIFORM_OCC void chachapoly_open_staged_vf(UniformArgs a)
+{
+    __shared__ uint4 tiles[4][512];
+    __shared__ FinSlot fin[4];
+    open_il_staged_vf<K, UKEY>(a, tiles[threadIdx.x >> 6], &fin[threadIdx.x >> 6], wave_of(blockIdx.x));
 }
 
 /* Duplex: one launch over two independent uniform jobs — seal job `s` and

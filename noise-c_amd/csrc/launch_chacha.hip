@@ -35,9 +35,9 @@ KernelFn<UniformArgs> chacha_staged_fn(bool open, bool ukey)
     return open ? chachapoly_open_staged<K, false> : chachapoly_seal_staged<K, false>;
 }
 
-/* vf: a VERIFY_FIRST open takes the one-lane kernel's AUTH + DEC passes
-   (open_solo_staged) or the two-pass chachapoly_open_uniform, never the
-   one-pass 4/8-lane staged kernels */
+/* vf: a VERIFY_FIRST open takes an AUTH + DEC kernel — the one-lane
+   open_solo_staged, the 4/8-lane open_il_staged_vf (FAST layouts) or the
+   two-pass chachapoly_open_uniform — never the one-pass staged kernels */
 template <bool FAST>
 KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf, bool runs)
 {
@@ -56,10 +56,12 @@ KernelFn<UniformArgs> chacha_uniform_fn_t(int k, bool open, bool ukey, bool vf, 
         return open ? chachapoly_open_uniform<1, FAST> : chachapoly_seal_uniform<1, FAST>;
     case 2: return open ? chachapoly_open_uniform<2, FAST> : chachapoly_seal_uniform<2, FAST>;
     case 4:
-        if (FAST && !(open && vf)) return chacha_staged_fn<4>(open, ukey);
+        if (FAST && open && vf) return ukey ? chachapoly_open_staged_vf<4, true> : chachapoly_open_staged_vf<4, false>;
+        if (FAST) return chacha_staged_fn<4>(open, ukey);
         return open ? chachapoly_open_uniform<4, FAST> : chachapoly_seal_uniform<4, FAST>;
     case 8:
-        if (FAST && !(open && vf)) return chacha_staged_fn<8>(open, ukey);
+        if (FAST && open && vf) return ukey ? chachapoly_open_staged_vf<8, true> : chachapoly_open_staged_vf<8, false>;
+        if (FAST) return chacha_staged_fn<8>(open, ukey);
         return open ? chachapoly_open_uniform<8, FAST> : chachapoly_seal_uniform<8, FAST>;
     case 16: return open ? chachapoly_open_uniform<16, FAST> : chachapoly_seal_uniform<16, FAST>;
     case 32: return open ? chachapoly_open_uniform<32, FAST> : chachapoly_seal_uniform<32, FAST>;
