@@ -749,6 +749,39 @@ NA_DEV void wave_dma(const UniformArgs &a, const WaveIO<K> &io, int j0, uint4 *t
             (lds_void *)(t + 64 * i), 16, 0, 0);
 }
 
+/* One LDS-DMA instruction (global_load_lds_dwordx4: lane l's 16 bytes land
+   at LDS address lds + 16 l), written as inline asm so that hipcc does not
+   see an LDS write: it would otherwise wait for the youngest such DMA before
+   every later LDS access of the wave (tile reads AND writes), i.e. for the
+   next step's DMA right after issuing it.  The one-lane kernels place their
+   own s_waitcnt vmcnt(0) instead (solo_wait).  m0 carries the LDS address:
+   m0 is reserved to the compiler (a clobber of it is not honoured), so the
+   statement saves and restores it (cdna_hip_programming.md, LDS-DMA
+   recipe) — the segmented kernels fault without that. */
+NA_DEV void dma16_asm(const void *g, uint32_t lds)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
+}
+
+/* The staged kernels' coalesced step DMA (wave_dma) issued as inline asm
+   (dma16_asm): hipcc does not see these LDS writes, so it does not wait for
+   the youngest of them before every tile read; the caller waits itself
+   (s_waitcnt vmcnt: four instructions per step). */
+template <int K>
+NA_DEV void wave_dma_asm(const UniformArgs &a, const WaveIO<K> &io, int j0, uint4 *t)
+{
+    const int u = j0 + io.kk;
+    const uint32_t off = io.d16 + 64u * (uint32_t)(u > 0 ? u : 0);
+    const uint32_t last = a.n_records - 1;
+    const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        dma16_asm((const void *)(a.in + (size_t)min(wave_rec(io, i), last) * a.in_stride + off),
+                  base + 1024u * (uint32_t)i);
+}
+
 /* A 16-B record store of the staged kernels: non-temporal (streaming), so
    the written lines need not displace the ciphertext lines the next step of
    an open still reads.  Round 4: the 4-lane kernels' standalone C2 seal+open
@@ -880,15 +913,16 @@ NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
     Mul mr, mjump;
     uint32_t s[4];
     bool seen = false;
-    wave_dma<K>(a, io, -(int)g.o - 1, tiles);
+    wave_dma_asm<K>(a, io, -(int)g.o - 1, tiles);
     for (uint32_t m = 0; m < g.steps; ++m) {
         if (a.balance) prio_by_progress(m, g.steps);
         const int j0 = (int)(m * K) - (int)g.o - 1;
         const int v = j0 + 1 + k;
         uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* last step's reads and writes of nxt are done */
         __builtin_amdgcn_wave_barrier();
         /* next step's bytes go into the other tile while this one computes */
-        if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
+        if (m + 1 < g.steps) wave_dma_asm<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
         slot_block<true>(key, pre, v, n_lo, n_hi, x, a.balance && 2 * m < g.steps);
         if (m == 0) {
@@ -902,6 +936,9 @@ NA_DEV void seal_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
             if (k == k0 && a.ad_len) poly_ad(acc, mr, u_ad(a, rc), a.ad_len);
         }
         __builtin_amdgcn_wave_barrier();
+        /* this step's DMA (a step old) landed; the next step's may still fly */
+        if (m + 1 < g.steps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t w[16];
         tile_get_unit(cur, lane, w);
 #pragma unroll
@@ -961,14 +998,15 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
     Mul mr, mjump;
     uint32_t s[4];
     bool seen = false;
-    wave_dma<K>(a, io, -(int)g.o - 1, tiles);
+    wave_dma_asm<K>(a, io, -(int)g.o - 1, tiles);
     for (uint32_t m = 0; m < g.steps; ++m) {
         if (a.balance) prio_by_progress(m, g.steps);
         const int j0 = (int)(m * K) - (int)g.o - 1;
         const int v = j0 + 1 + k;
         uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* last step's reads and writes of nxt are done */
         __builtin_amdgcn_wave_barrier();
-        if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
+        if (m + 1 < g.steps) wave_dma_asm<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
         slot_block<true>(key, pre, v, n_lo, n_hi, x, a.balance && 2 * m < g.steps);
         if (m == 0) {
@@ -982,6 +1020,9 @@ NA_DEV void open_il_staged(const UniformArgs &a, uint4 *tiles, FinSlot *fin, uin
             if (k == k0 && a.ad_len) poly_ad(acc, mr, u_ad(a, rc), a.ad_len);
         }
         __builtin_amdgcn_wave_barrier();
+        /* this step's DMA (a step old) landed; the next step's may still fly */
+        if (m + 1 < g.steps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t w[16];
         tile_get_unit(cur, lane, w);
         if (v >= 1 && (uint32_t)v <= g.J) {
@@ -1072,22 +1113,6 @@ NA_DEV uint32_t solo_slot(uint32_t L, uint32_t c) { return L * 8 + (c ^ (L & 7))
 /* chunk this lane moves in a coalesced instruction (slot 64i + lane holds
    owner 8i + lane/8, chunk (lane ^ lane/8) & 7) */
 NA_DEV uint32_t solo_chunk(uint32_t lane) { return (lane ^ (lane >> 3)) & 7; }
-
-/* One LDS-DMA instruction (global_load_lds_dwordx4: lane l's 16 bytes land
-   at LDS address lds + 16 l), written as inline asm so that hipcc does not
-   see an LDS write: it would otherwise wait for the youngest such DMA before
-   every later LDS access of the wave (tile reads AND writes), i.e. for the
-   next step's DMA right after issuing it.  The one-lane kernels place their
-   own s_waitcnt vmcnt(0) instead (solo_wait).  m0 carries the LDS address:
-   m0 is reserved to the compiler (a clobber of it is not honoured), so the
-   statement saves and restores it (cdna_hip_programming.md, LDS-DMA
-   recipe) — the segmented kernels fault without that. */
-NA_DEV void dma16_asm(const void *g, uint32_t lds)
-{
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(lds) : "memory");
-}
 
 /* every vector-memory operation of the wave done (the DMA into the tile
    about to be read, issued a step earlier, and the stores issued with it) */
@@ -1746,23 +1771,6 @@ NA_DEV RecView ragged_view(const RaggedArgs &a, uint32_t rec)
 NA_DEV uint32_t wave_of(uint32_t b) { return (b * 256u + threadIdx.x) >> 6; }
 
 /* LDS-staged uniform FAST batches, K = 4 or 8 lanes per record */
-/* The staged kernels' coalesced step DMA (wave_dma) issued as inline asm
-   (dma16_asm): hipcc does not see these LDS writes, so it does not wait for
-   the youngest of them before every tile read; the caller waits itself
-   (s_waitcnt vmcnt: four instructions per step). */
-template <int K>
-NA_DEV void wave_dma_asm(const UniformArgs &a, const WaveIO<K> &io, int j0, uint4 *t)
-{
-    const int u = j0 + io.kk;
-    const uint32_t off = io.d16 + 64u * (uint32_t)(u > 0 ? u : 0);
-    const uint32_t last = a.n_records - 1;
-    const uint32_t base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void *)t);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        dma16_asm((const void *)(a.in + (size_t)min(wave_rec(io, i), last) * a.in_stride + off),
-                  base + 1024u * (uint32_t)i);
-}
-
 /* Verify-first open with K lanes per record (round 6): the reference's order
    (cipher-chachapoly.c:135-141) at the staged kernels' four waves per SIMD,
    for standalone opens (the one-lane verify-first open holds one wave per
@@ -1848,14 +1856,15 @@ NA_DEV void open_il_staged_vf(const UniformArgs &a, uint4 *tiles, FinSlot *fin, 
     for (int i = 0; i < 4; ++i)
         okm |= (__shfl((int)ok, (int)(16u * i + (lane >> 2)), 64) != 0 ? 1u : 0u) << i;
     __builtin_amdgcn_wave_barrier(); /* the AUTH pass's tile reads are done */
-    wave_dma<K>(a, io, -(int)g.o - 1, tiles);
+    wave_dma_asm<K>(a, io, -(int)g.o - 1, tiles);
     for (uint32_t m = 0; m < g.steps; ++m) {
         if (a.balance) prio_by_progress(m, g.steps);
         const int j0 = (int)(m * K) - (int)g.o - 1;
         const int v = j0 + 1 + k;
         uint4 *cur = tiles + 256 * (m & 1), *nxt = tiles + 256 * ((m + 1) & 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* last step's reads and writes of nxt are done */
         __builtin_amdgcn_wave_barrier();
-        if (m + 1 < g.steps) wave_dma<K>(a, io, j0 + K, nxt);
+        if (m + 1 < g.steps) wave_dma_asm<K>(a, io, j0 + K, nxt);
         uint32_t x[16];
         if (m == 0) {
 #pragma unroll
@@ -1864,6 +1873,9 @@ NA_DEV void open_il_staged_vf(const UniformArgs &a, uint4 *tiles, FinSlot *fin, 
             slot_block<true>(key, pre, v, n_lo, n_hi, x, a.balance && 2 * m < g.steps);
         }
         __builtin_amdgcn_wave_barrier();
+        /* this step's DMA (a step old) landed; the next step's may still fly */
+        if (m + 1 < g.steps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t w[16];
         tile_get_unit(cur, lane, w);
 #pragma unroll
