@@ -257,3 +257,82 @@ def test_full_size_duplex_at_bench_slots(name, lanes, vf):
     fill = 0xA5 if (vf or cipher == A.AESGCM) else 0
     assert int(bv[~good].max().item()) == fill
     assert int(bv[~good].min().item()) == fill
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,vf,in_place", [("c2", True, False), ("c2", True, True), ("c2", False, False),
+                                              ("perf", True, False)])
+def test_full_size_standalone_open_at_bench_slots(name, vf, in_place):
+    """The standalone opens of the bench's per-direction pass and --mode
+    separate at full size and the bench slots: since round 6 a verify-first
+    open of 64 Ki FAST records runs four lanes per record
+    (chachapoly_open_staged_vf<4, true>); with NOISE_AEAD_FLAG_ONE_PASS the
+    one-pass chachapoly_open_staged<4, true>.  A batch sealed by the library
+    (its sealed digest checked against the golden one) with 64 records
+    tampered: every other record opens to the plaintext, the tampered ones
+    get status 1 and are never written (verify-first: out of place the fill
+    stays, in place the ciphertext stays) or zeroed (one pass, out of
+    place)."""
+    import torch
+
+    import noise_aead as A
+    A.lib()
+    c = _golden()[name]
+    N, L, cipher, S, AD = c["records"], c["len"], c["cipher"], c["states"], c.get("ad", 0)
+    ins, outs = (L + 127) // 128 * 128, (L + 16 + 127) // 128 * 128
+    gins = c["in_stride"]
+    sp = torch.cuda.current_stream().cuda_stream
+    raw = torch.empty(S * 32, dtype=torch.uint8, device="cuda")
+    for k in range(S):
+        assert A.dev_fill_splitmix(raw[32 * k:].data_ptr(), 32, SEED_KEY, 4 * k, sp) == 0
+    ctx = torch.empty(S * A.dev_ctx_bytes(cipher), dtype=torch.uint8, device="cuda")
+    assert A.dev_prepare(cipher, raw.data_ptr(), S, ctx.data_ptr(), sp) == 0
+    nb = torch.zeros(S, dtype=torch.int64, device="cuda")
+    gpt = torch.empty(N * gins, dtype=torch.uint8, device="cuda")
+    assert A.dev_fill_splitmix(gpt.data_ptr(), gpt.numel(), SEED_PT, 0, sp) == 0
+    pt = torch.zeros(N * ins, dtype=torch.uint8, device="cuda")
+    pt.view(N, ins)[:, :L] = gpt.view(N, gins)[:, :L]
+    del gpt
+    ad_kw = {}
+    if AD:
+        adb = torch.empty(N * AD, dtype=torch.uint8, device="cuda")
+        assert A.dev_fill_splitmix(adb.data_ptr(), adb.numel(), 0x6164, 0, sp) == 0
+        ad_kw = dict(ad=adb.data_ptr(), ad_stride=AD, ad_len=AD)
+    common = dict(ctx=ctx.data_ptr(), nonce_base=nb.data_ptr(), length=L, n_records=N,
+                  recs_per_state=N // S, **ad_kw)
+    ct = torch.empty(N * outs, dtype=torch.uint8, device="cuda")
+    assert A.dev_uniform(False, cipher, inp=pt.data_ptr(), out=ct.data_ptr(), in_stride=ins,
+                         out_stride=outs, stream=sp, **common) == 0
+    torch.cuda.synchronize()
+    sealed = ct.view(N, outs)[:, :L + 16].contiguous().cpu().numpy()
+    assert hashlib.sha256(sealed.tobytes()).hexdigest() == c["sealed_sha256"], name
+    del sealed
+    rng = np.random.default_rng(29 + 2 * vf + in_place)
+    bad = np.unique(rng.integers(0, N, 64))
+    pos = torch.from_numpy(bad * outs + rng.integers(0, L + 16, len(bad))).to("cuda")
+    ct.view(-1)[pos] ^= 0x40
+    tampered = ct.clone()
+    st = torch.full((N,), 9, dtype=torch.uint8, device="cuda")
+    if in_place:
+        out, out_stride = ct, outs
+    else:
+        out, out_stride = torch.full((N * ins,), 0xA5, dtype=torch.uint8, device="cuda"), ins
+    assert A.dev_uniform(True, cipher, inp=ct.data_ptr(), out=out.data_ptr(), in_stride=outs,
+                         out_stride=out_stride, status=st.data_ptr(),
+                         flags=0 if vf else A.FLAG_ONE_PASS, stream=sp, **common) == 0
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    exp = np.zeros(N, dtype=np.uint8)
+    exp[bad] = 1
+    assert np.array_equal(s, exp), np.nonzero(s != exp)[0][:10]
+    good = torch.ones(N, dtype=torch.bool, device="cuda")
+    good[torch.from_numpy(bad).to("cuda")] = False
+    bv = out.view(N, out_stride)
+    assert torch.equal(bv[good][:, :L], pt.view(N, ins)[:, :L][good])
+    if in_place:  # rejected: the ciphertext and tag as given
+        tv = tampered.view(N, outs)[:, :L + 16]
+        assert torch.equal(bv[~good][:, :L + 16], tv[~good])
+    else:
+        fill = 0xA5 if vf else 0
+        assert int(bv[~good][:, :L].max().item()) == fill
+        assert int(bv[~good][:, :L].min().item()) == fill
