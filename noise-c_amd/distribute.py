@@ -11,7 +11,12 @@ to it:
 - ``gather_records``: the reverse, every rank's output slice lands at its
   offset of the destination rank's flat buffer.
 
-Both are single ``torch.distributed`` scatter/gather calls, which the nccl
+- ``scatter_records_v`` / ``gather_records_v``: the same for shards of
+  different sizes (C5's ragged shards), packed back to back in the flat
+  buffer — one point-to-point send/receive per peer in one batch, so no
+  shard travels padded to the largest one's size.
+
+The equal-size pair are single ``torch.distributed`` scatter/gather calls, which the nccl
 backend (RCCL on ROCm) runs as grouped ncclSend/ncclRecv over xGMI — one
 point-to-point transfer per peer, all peers in flight at once, matching the
 "scatter inputs / gather outputs" shape the north star names.  On CPU tensors
@@ -58,3 +63,68 @@ def gather_records(local, full: Optional[object], dst: int = 0, group=None) -> N
             raise ValueError("the destination rank must pass the full buffer")
         parts = _slices(full, world, local.numel())
     dist.gather(local, gather_list=parts, dst=dst, group=group)
+
+
+def _offsets(sizes):
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += int(n)
+    return offs, o
+
+
+def _p2p(ops) -> None:
+    import torch.distributed as dist
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+
+def scatter_records_v(local, full: Optional[object], sizes, src: int = 0, group=None) -> None:
+    """Variable-size scatter: rank r receives ``sizes[r]`` bytes into
+    ``local[:sizes[r]]`` from offset sum(sizes[:r]) of ``full`` (the shards
+    packed back to back, read on ``src`` only).  Every rank calls it (one
+    batched send per peer on ``src``, one receive elsewhere)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(sizes) != world:
+        raise ValueError(f"{len(sizes)} shard sizes for {world} ranks")
+    if local.dim() != 1 or not local.is_contiguous() or local.numel() < int(sizes[rank]):
+        raise ValueError("local shard must be a flat contiguous tensor of at least its size")
+    offs, total = _offsets(sizes)
+    ops = []
+    if rank == src:
+        if full is None or full.numel() < total:
+            raise ValueError("the source rank must pass the packed buffer of every shard")
+        for r in range(world):
+            if r != src and sizes[r]:
+                ops.append(dist.P2POp(dist.isend, full[offs[r]:offs[r] + int(sizes[r])], r, group))
+        local[:int(sizes[src])].copy_(full[offs[src]:offs[src] + int(sizes[src])])
+    elif sizes[rank]:
+        ops.append(dist.P2POp(dist.irecv, local[:int(sizes[rank])], src, group))
+    _p2p(ops)
+
+
+def gather_records_v(local, full: Optional[object], sizes, dst: int = 0, group=None) -> None:
+    """Variable-size gather: ``local[:sizes[r]]`` of every rank r lands at
+    offset sum(sizes[:r]) of ``full`` on ``dst`` (packed, no padding)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(sizes) != world:
+        raise ValueError(f"{len(sizes)} shard sizes for {world} ranks")
+    if local.dim() != 1 or not local.is_contiguous() or local.numel() < int(sizes[rank]):
+        raise ValueError("local shard must be a flat contiguous tensor of at least its size")
+    offs, total = _offsets(sizes)
+    ops = []
+    if rank == dst:
+        if full is None or full.numel() < total:
+            raise ValueError("the destination rank must pass the packed buffer of every shard")
+        for r in range(world):
+            if r != dst and sizes[r]:
+                ops.append(dist.P2POp(dist.irecv, full[offs[r]:offs[r] + int(sizes[r])], r, group))
+        full[offs[dst]:offs[dst] + int(sizes[dst])].copy_(local[:int(sizes[dst])])
+    elif sizes[rank]:
+        ops.append(dist.P2POp(dist.isend, local[:int(sizes[rank])], dst, group))
+    _p2p(ops)

@@ -124,6 +124,53 @@ def test_two_rank_scatter_seal_gather():
     assert got == expect
 
 
+def _xfer_v_worker(rank, world, port, sizes, q):
+    """Variable-size scatter/gather (C5's ragged shards) on gloo: shards
+    packed back to back, no padding; every rank transforms its shard (byte
+    + rank + 1) and rank 0 gathers them back."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.join(ROOT, "noise-c_amd"))
+    from distribute import gather_records_v, scatter_records_v
+    total = sum(sizes)
+    full_in = full_out = None
+    if rank == 0:
+        full_in = torch.arange(total, dtype=torch.int64).remainder(251).to(torch.uint8)
+        full_out = torch.zeros(total, dtype=torch.uint8)
+    local = torch.full((max(sizes) + 5,), 0xEE, dtype=torch.uint8)  # larger than the shard
+    scatter_records_v(local, full_in, sizes, src=0)
+    off = sum(sizes[:rank])
+    exp = torch.arange(off, off + sizes[rank], dtype=torch.int64).remainder(251).to(torch.uint8)
+    assert torch.equal(local[:sizes[rank]], exp)
+    assert int(local[sizes[rank]:].min()) == 0xEE  # nothing past the shard written
+    local[:sizes[rank]] += rank + 1
+    gather_records_v(local, full_out, sizes, dst=0)
+    if rank == 0:
+        q.put(bytes(full_out.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes", [[1000, 1737], [0, 64, 5, 300]])
+def test_variable_size_scatter_gather(sizes):
+    world = len(sizes)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 1000 + 7 * world
+    procs = [ctx.Process(target=_xfer_v_worker, args=(r, world, port, sizes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = bytearray()
+    for r, n in enumerate(sizes):
+        off = sum(sizes[:r])
+        expect += bytes(((i % 251) + r + 1) % 256 for i in range(off, off + n))
+    assert got == bytes(expect)
+
+
 def test_c4_strong_shards_equal_one_gpu_layout():
     """C4 is strong scaling (bench.py: records and states divided by N): the
     ranks' (state key id, nonce) sets of N = 2 and 4 are exactly the N = 1
